@@ -1,0 +1,165 @@
+/*
+ * rfa.h -- C-ABI of the MI355X-native RFAnalyzer spectrum pipeline (librfa.so).
+ *
+ * Replaces the reference's spectrum hot path (thomasjoergensen/RFAnalyzer):
+ *
+ *   reference interface                                   replaced by
+ *   ----------------------------------------------------  -------------------------------------
+ *   NativeDsp.performWindowedFftAndReturnMag(re,im,mag)    rfa_windowed_fft_mag_planar()
+ *     nativedsp/src/main/java/com/mantz_it/nativedsp/NativeDsp.kt:43-62
+ *   JNI performFFTAndLogMag(in[2N], out[N])                rfa_fft_logmag_interleaved()
+ *     nativedsp/src/main/cpp/nativedsp.cpp:44-81
+ *   JNI performFFT(in[2N], out[2N])                        rfa_fft_ordered()
+ *     nativedsp/src/main/cpp/nativedsp.cpp:19-42
+ *   IQConverter.fillPacketIntoSamplePacket + window + FFT  rfa_process() / rfa_process_host()
+ *     source/Signed8BitIQConverter.java:80-99,                (raw IQ bytes in, fused on device)
+ *     Unsigned8BitIQConverter.java:80-99,
+ *     Signed16BitIQConverter.kt:89-124, Scheduler.kt:252-279
+ *   FftProcessor.run ring write / retune shift / peak-hold rfa_process(), rfa_set_tuning(),
+ *     analyzer/FftProcessor.kt:164-245                        rfa_get_ring(), rfa_get_peaks()
+ *   AnalyzerSurface boxcar time average                    rfa_get_boxcar()
+ *     ui/AnalyzerSurface.kt:657-714
+ *   (north-star extension) exponential average             rfa_get_ema()
+ *     idiom of database/GlobalPerformanceData.kt:44-50
+ *
+ * (app paths are relative to app/src/main/java/com/mantz_it/rfanalyzer/.)
+ *
+ * Conventions
+ *  - Every function returns an int status: RFA_OK (0) or a negative RFA_ERR_*.
+ *  - A handle is single-threaded; separate handles are independent (one per
+ *    GPU / HIP stream).  There is no process-global state.
+ *  - Output rows are 10*log10(|X_k|/N) (nativedsp.cpp:78), fft-shifted so that
+ *    out[t] holds bin (t + N/2) mod N (out[0] = -fs/2, out[N/2] = DC).
+ *  - N is a power of two, RFA_MIN_FFT_SIZE..RFA_MAX_FFT_SIZE.
+ *  - Device pointers are HIP device (or host-coherent) addresses; work is
+ *    enqueued on the handle's stream and is asynchronous unless the function
+ *    name ends in _host or the doc says it synchronises.
+ */
+#ifndef RFA_H
+#define RFA_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef RFA_API
+#define RFA_API __attribute__((visibility("default")))
+#endif
+
+#define RFA_ABI_VERSION 1
+#define RFA_MIN_FFT_SIZE 64
+#define RFA_MAX_FFT_SIZE (1 << 20)
+
+enum rfa_status {
+    RFA_OK = 0,
+    RFA_ERR_INVALID = -1,     /* NULL handle/pointer, bad enum, bad size  */
+    RFA_ERR_SIZE = -2,        /* array length mismatch (NativeDsp.kt:45-46) */
+    RFA_ERR_UNSUPPORTED = -3, /* fft size / mode not supported             */
+    RFA_ERR_NODEVICE = -4,    /* no HIP device visible                     */
+    RFA_ERR_NOMEM = -5,       /* device / host allocation failed           */
+    RFA_ERR_HIP = -6,         /* HIP runtime error (see rfa_last_error)    */
+    RFA_ERR_STATE = -7        /* operation needs a feature not enabled     */
+};
+
+enum rfa_window { RFA_WINDOW_BLACKMAN = 0, RFA_WINDOW_HANN = 1, RFA_WINDOW_NONE = 2 };
+
+/* Raw IQ sample formats (IQ_FILE_FORMAT.md / the converters above). */
+enum rfa_input_format {
+    RFA_IN_S8 = 0,             /* HackRF: int8 I,Q        -> b/128            */
+    RFA_IN_U8 = 1,             /* RTL-SDR: uint8 I,Q      -> (b-127.4f)/128   */
+    RFA_IN_S16LE = 2,          /* Airspy/HydraSDR: int16  -> s/32768          */
+    RFA_IN_F32_INTERLEAVED = 3,/* float I,Q                                   */
+    RFA_IN_F32_PLANAR = 4      /* per frame: float re[N] then float im[N]     */
+};
+
+enum rfa_avg_mode { RFA_AVG_NONE = 0, RFA_AVG_BOXCAR = 1, RFA_AVG_EMA = 2 };
+
+typedef struct rfa_config {
+    int32_t fft_size;      /* N, power of two                                       */
+    int32_t window;        /* enum rfa_window                                       */
+    int32_t input_format;  /* enum rfa_input_format                                 */
+    int32_t avg_mode;      /* enum rfa_avg_mode (boxcar reads the ring)             */
+    int32_t avg_length;    /* boxcar: L (average of the newest L+1 rows), 0..ring   */
+    float ema_alpha;       /* EMA: avg += alpha*(x-avg), 0 < alpha <= 1             */
+    int32_t peak_hold;     /* 0/1 (FftProcessor.kt:229-245)                         */
+    int32_t ring_rows;     /* waterfall rows R (500/400/300, FftProcessor.kt:103), 0 = no ring */
+    int32_t device_id;     /* HIP device ordinal                                    */
+} rfa_config;
+
+typedef struct rfa_handle rfa_handle;
+
+/* Library / device queries (no handle). */
+RFA_API int rfa_abi_version(void);
+RFA_API int rfa_device_count(int *count);
+RFA_API const char *rfa_status_string(int status);
+RFA_API void rfa_default_config(rfa_config *cfg); /* N=16384, Blackman, s8, no avg, no peak, 400 rows, dev 0 */
+
+/* Lifetime. */
+RFA_API int rfa_create(const rfa_config *cfg, rfa_handle **out);
+RFA_API int rfa_destroy(rfa_handle *h);
+RFA_API int rfa_get_config(const rfa_handle *h, rfa_config *cfg);
+RFA_API const char *rfa_last_error(const rfa_handle *h);
+
+/* Stream control: `stream` is a hipStream_t (NULL = the handle's own stream). */
+RFA_API int rfa_set_stream(rfa_handle *h, void *stream);
+RFA_API int rfa_get_stream(const rfa_handle *h, void **stream);
+RFA_API int rfa_synchronize(rfa_handle *h);
+
+/* Batch processing.  `in` holds n_frames frames of N samples in the configured
+ * format, frame f starting at byte f*frame_stride_bytes (0 = densely packed).
+ * For a headerless file replayed in packets of P bytes with N <= P/bps, the
+ * reference's framing (Scheduler.kt:252-279: each packet fills one frame,
+ * the rest of the packet is dropped) is frame_stride_bytes = P.
+ * Rows go to `rows` (n_frames*N floats, frame order; may be NULL) and, if
+ * ring_rows > 0, into the device waterfall ring in the reference's reverse
+ * order (frames of this batch that the reference would overwrite within the
+ * same batch are not stored).  Peak-hold / EMA state advance frame by frame.
+ *   rfa_process      : device pointers, asynchronous on the handle stream.
+ *   rfa_process_host : host pointers; copies in/out and synchronises. */
+RFA_API int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
+RFA_API int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
+
+/* Tuning metadata of the following frames (SamplePacket.frequency/sampleRate).
+ * Mirrors FftProcessor.kt:169-220,238-239: a frequency change shifts every ring
+ * row by (int)((f_old-f_new)*(N/(float)sr)) bins with -9999 fill (or clears it
+ * when |shift| >= N); a sample-rate change clears the ring; either resets the
+ * peaks and the EMA.  The first call only records the values (the ring starts
+ * cleared). */
+RFA_API int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate);
+
+/* State read-back (synchronise the handle stream; host destination).
+ * rfa_get_ring copies ring_rows*N floats in storage order and returns the
+ * reference's readIndex (newest row) and writeIndex (FftProcessorData). */
+RFA_API int rfa_get_peaks(rfa_handle *h, float *out);
+RFA_API int rfa_get_ema(rfa_handle *h, float *out);
+RFA_API int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out);
+RFA_API int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_index);
+RFA_API int rfa_reset_state(rfa_handle *h); /* ring -> -9999, peaks/EMA -> uninitialised */
+
+/* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers. */
+RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);
+
+/* Reference-seam entry points (host arrays, synchronous).  They use the
+ * handle's N; the window/format of the handle are ignored where the reference
+ * symbol fixes them. */
+/* NativeDsp.kt:43-62: Blackman-windowed FFT of planar re/im, log-mag row out.
+ * Returns RFA_ERR_SIZE on length mismatch (the Kotlin method returns false). */
+RFA_API int rfa_windowed_fft_mag_planar(rfa_handle *h, const float *re, const float *im, float *mag_out, size_t n);
+/* nativedsp.cpp:44-81: already-windowed interleaved input (2N floats) -> N dB. */
+RFA_API int rfa_fft_logmag_interleaved(rfa_handle *h, const float *in, float *mag_out, size_t n);
+/* nativedsp.cpp:19-42: ordered, unscaled, forward complex FFT, 2N floats each. */
+RFA_API int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n);
+
+/* Profiling: when enabled, HIP events bracket every main FFT kernel launch on
+ * the handle stream and the summed device time is reported. */
+RFA_API int rfa_set_profiling(rfa_handle *h, int enable);
+RFA_API int rfa_get_kernel_time(rfa_handle *h, double *total_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RFA_H */

@@ -1,0 +1,681 @@
+// librfa engine: the handle-based C-ABI of include/rfa.h.
+//
+// A handle is the native counterpart of one reference FftProcessor + NativeDsp
+// pair (analyzer/FftProcessor.kt:64-257, nativedsp/.../NativeDsp.kt): it owns a
+// HIP stream, the device-resident window and twiddle tables, the waterfall
+// ring, peak-hold and EMA state, and the ring bookkeeping (writeIndex /
+// readIndex / last frequency and sample rate).  No process-global state.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rfa.h"
+#include "fft_kernels.h"
+
+using rfa::FftLaunch;
+
+struct rfa_handle {
+    rfa_config cfg{};
+    int n = 0, logn = 0;
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    float *d_window = nullptr;
+    float *d_window_none = nullptr;  // all ones (already-windowed seams)
+    float2 *d_twc = nullptr, *d_twf = nullptr;
+    int tw_shift = 0;
+    float *d_ring = nullptr, *d_ring_tmp = nullptr;
+    int ring_rows = 0;
+    int write_index = 0, read_index = 0;
+    bool have_rows = false;  // at least one row pushed since the last reset
+    float *d_peaks = nullptr;
+    float *d_ema = nullptr;
+    float *d_boxcar = nullptr;
+    bool have_tuning = false;
+    int64_t last_frequency = 0, last_sample_rate = 0;
+    // staging for host-pointer entry points / state without a row buffer
+    void *d_in = nullptr;
+    size_t d_in_cap = 0;
+    float *d_rows = nullptr;
+    size_t d_rows_cap = 0;
+    void *h_pinned = nullptr;
+    size_t h_pinned_cap = 0;
+    // profiling
+    bool profile = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    double kernel_ms = 0.0;
+    int64_t launches = 0;
+    std::string err;
+};
+
+namespace {
+
+constexpr float kRingFill = -9999.0f;     // FftProcessor.kt:180
+constexpr float kPeakFill = -999999.0f;   // FftProcessor.kt:235
+
+int fail(rfa_handle *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    return code;
+}
+
+int hip_fail(rfa_handle *h, hipError_t e, const char *where) {
+    return fail(h, RFA_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(h, expr)                                      \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail((h), _e, #expr); \
+    } while (0)
+
+int ilog2_exact(int n) {
+    if (n <= 0) return -1;
+    int l = 0;
+    while ((1 << l) < n) l++;
+    return (1 << l) == n ? l : -1;
+}
+
+size_t bytes_per_sample(int fmt) {
+    switch (fmt) {
+    case RFA_IN_S8:
+    case RFA_IN_U8: return 2;
+    case RFA_IN_S16LE: return 4;
+    case RFA_IN_F32_INTERLEAVED:
+    case RFA_IN_F32_PLANAR: return 8;
+    default: return 0;
+    }
+}
+
+size_t load_alignment(int fmt) {
+    switch (fmt) {
+    case RFA_IN_S8:
+    case RFA_IN_U8: return 2;
+    case RFA_IN_S16LE: return 4;
+    case RFA_IN_F32_INTERLEAVED: return 8;
+    default: return 4;
+    }
+}
+
+// NativeDsp.kt:14-21: Blackman in double, cast once; Hann with the same (N-1) convention.
+std::vector<float> make_window(int n, int kind) {
+    std::vector<float> w(n);
+    for (int i = 0; i < n; i++) {
+        const double x = 2.0 * M_PI * (double)i / (double)(n - 1);
+        double v = 1.0;
+        if (kind == RFA_WINDOW_BLACKMAN) v = 0.42 - 0.5 * std::cos(x) + 0.08 * std::cos(2.0 * x);
+        else if (kind == RFA_WINDOW_HANN) v = 0.5 - 0.5 * std::cos(x);
+        w[i] = (float)v;
+    }
+    return w;
+}
+
+int ensure_device_buffer(rfa_handle *h, void **p, size_t *cap, size_t bytes) {
+    if (*cap >= bytes) return RFA_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc(p, bytes) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "hipMalloc staging");
+    *cap = bytes;
+    return RFA_OK;
+}
+
+int ensure_pinned(rfa_handle *h, size_t bytes) {
+    if (h->h_pinned_cap >= bytes) return RFA_OK;
+    if (h->h_pinned) hipHostFree(h->h_pinned);
+    h->h_pinned = nullptr;
+    h->h_pinned_cap = 0;
+    if (hipHostMalloc(&h->h_pinned, bytes, hipHostMallocDefault) != hipSuccess)
+        return fail(h, RFA_ERR_NOMEM, "hipHostMalloc staging");
+    h->h_pinned_cap = bytes;
+    return RFA_OK;
+}
+
+int set_device(rfa_handle *h) {
+    hipError_t e = hipSetDevice(h->device);
+    if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
+    return RFA_OK;
+}
+
+// Collect finished profiling event pairs.
+void drain_events(rfa_handle *h, bool wait) {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> keep;
+    for (auto &pr : h->ev_pending) {
+        if (wait) hipEventSynchronize(pr.second);
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+            h->kernel_ms += ms;
+            h->launches++;
+            h->ev_pool.push_back(pr.first);
+            h->ev_pool.push_back(pr.second);
+        } else {
+            keep.push_back(pr);
+        }
+    }
+    h->ev_pending.swap(keep);
+}
+
+hipEvent_t get_event(rfa_handle *h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    hipEventCreate(&e);
+    return e;
+}
+
+int launch_main(rfa_handle *h, FftLaunch &a) {
+    a.stream = h->stream;
+    a.logn = h->logn;
+    a.tw_coarse = h->d_twc;
+    a.tw_fine = h->d_twf;
+    a.tw_shift = h->tw_shift;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->profile) {
+        if (h->ev_pending.size() > 256) drain_events(h, true);
+        e0 = get_event(h);
+        e1 = get_event(h);
+        hipEventRecord(e0, h->stream);
+    }
+    hipError_t e = rfa::launch_fft(a);
+    if (h->profile) {
+        hipEventRecord(e1, h->stream);
+        h->ev_pending.emplace_back(e0, e1);
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "launch_fft");
+    return RFA_OK;
+}
+
+int clear_ring(rfa_handle *h) {
+    if (!h->d_ring) return RFA_OK;
+    HIPCHK(h, rfa::launch_fill(h->d_ring, (long long)h->ring_rows * h->n, kRingFill, h->stream));
+    return RFA_OK;
+}
+
+int reset_peaks_ema(rfa_handle *h) {
+    if (h->d_peaks) HIPCHK(h, rfa::launch_fill(h->d_peaks, h->n, kPeakFill, h->stream));
+    if (h->d_ema) HIPCHK(h, rfa::launch_fill(h->d_ema, h->n, -INFINITY, h->stream));
+    return RFA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rfa_abi_version(void) { return RFA_ABI_VERSION; }
+
+int rfa_device_count(int *count) {
+    if (!count) return RFA_ERR_INVALID;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return RFA_OK;
+}
+
+const char *rfa_status_string(int status) {
+    switch (status) {
+    case RFA_OK: return "ok";
+    case RFA_ERR_INVALID: return "invalid argument";
+    case RFA_ERR_SIZE: return "size mismatch";
+    case RFA_ERR_UNSUPPORTED: return "unsupported";
+    case RFA_ERR_NODEVICE: return "no HIP device";
+    case RFA_ERR_NOMEM: return "out of memory";
+    case RFA_ERR_HIP: return "HIP runtime error";
+    case RFA_ERR_STATE: return "feature not enabled";
+    default: return "unknown status";
+    }
+}
+
+void rfa_default_config(rfa_config *c) {
+    if (!c) return;
+    std::memset(c, 0, sizeof(*c));
+    c->fft_size = 16384;  // AppStateRepository.kt:196
+    c->window = RFA_WINDOW_BLACKMAN;
+    c->input_format = RFA_IN_S8;
+    c->avg_mode = RFA_AVG_NONE;
+    c->avg_length = 0;  // AppStateRepository.kt:197
+    c->ema_alpha = 0.1f;
+    c->peak_hold = 0;     // AppStateRepository.kt:198
+    c->ring_rows = 400;   // waterfallSpeed NORMAL, FftProcessor.kt:103
+    c->device_id = 0;
+}
+
+int rfa_create(const rfa_config *cfg, rfa_handle **out) {
+    if (!cfg || !out) return RFA_ERR_INVALID;
+    *out = nullptr;
+    const int logn = ilog2_exact(cfg->fft_size);
+    if (logn < 0 || cfg->fft_size < RFA_MIN_FFT_SIZE || cfg->fft_size > RFA_MAX_FFT_SIZE) return RFA_ERR_UNSUPPORTED;
+    if (logn > rfa::kMaxLogM + rfa::kMaxLogSplit) return RFA_ERR_UNSUPPORTED;  // two-pass large-N path pending
+    if (cfg->window < 0 || cfg->window > RFA_WINDOW_NONE) return RFA_ERR_INVALID;
+    if (bytes_per_sample(cfg->input_format) == 0) return RFA_ERR_INVALID;
+    if (cfg->avg_mode < RFA_AVG_NONE || cfg->avg_mode > RFA_AVG_EMA) return RFA_ERR_INVALID;
+    if (cfg->avg_mode == RFA_AVG_EMA && !(cfg->ema_alpha > 0.f && cfg->ema_alpha <= 1.f)) return RFA_ERR_INVALID;
+    if (cfg->ring_rows < 0 || cfg->avg_length < 0) return RFA_ERR_INVALID;
+    if (cfg->avg_mode == RFA_AVG_BOXCAR && cfg->avg_length >= std::max(cfg->ring_rows, 1)) return RFA_ERR_INVALID;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return RFA_ERR_NODEVICE;
+    if (cfg->device_id < 0 || cfg->device_id >= ndev) return RFA_ERR_NODEVICE;
+
+    rfa_handle *h = new (std::nothrow) rfa_handle();
+    if (!h) return RFA_ERR_NOMEM;
+    h->cfg = *cfg;
+    h->n = cfg->fft_size;
+    h->logn = logn;
+    h->device = cfg->device_id;
+    h->ring_rows = cfg->ring_rows;
+    int rc = set_device(h);
+    if (rc) { delete h; return rc; }
+    auto bail = [&](int code) { rfa_destroy(h); return code; };
+    if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RFA_ERR_HIP);
+    h->stream = h->own_stream;
+
+    const int n = h->n;
+    // window tables
+    std::vector<float> w = make_window(n, cfg->window), ones(n, 1.0f);
+    if (hipMalloc(&h->d_window, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (hipMalloc(&h->d_window_none, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (hipMemcpy(h->d_window, w.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
+    if (hipMemcpy(h->d_window_none, ones.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+        return bail(RFA_ERR_HIP);
+    // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
+    // rounded from double (no device sin/cos)
+    h->tw_shift = (logn + 1) / 2;
+    const int nc = n >> h->tw_shift, nf = 1 << h->tw_shift;
+    std::vector<float2> tc(nc), tf(nf);
+    for (int c = 0; c < nc; c++) {
+        const double a = -2.0 * M_PI * (double)((long long)c << h->tw_shift) / (double)n;
+        tc[c] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    for (int f = 0; f < nf; f++) {
+        const double a = -2.0 * M_PI * (double)f / (double)n;
+        tf[f] = make_float2((float)std::cos(a), (float)std::sin(a));
+    }
+    if (hipMalloc(&h->d_twc, nc * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (hipMalloc(&h->d_twf, nf * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (hipMemcpy(h->d_twc, tc.data(), nc * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
+    if (hipMemcpy(h->d_twf, tf.data(), nf * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
+    // state
+    if (h->ring_rows > 0) {
+        const size_t bytes = (size_t)h->ring_rows * n * sizeof(float);
+        if (hipMalloc(&h->d_ring, bytes) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMalloc(&h->d_ring_tmp, bytes) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    }
+    if (cfg->peak_hold && hipMalloc(&h->d_peaks, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (cfg->avg_mode == RFA_AVG_EMA && hipMalloc(&h->d_ema, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (hipMalloc(&h->d_boxcar, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (clear_ring(h) || reset_peaks_ema(h)) return bail(RFA_ERR_HIP);
+    if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(RFA_ERR_HIP);
+    *out = h;
+    return RFA_OK;
+}
+
+int rfa_destroy(rfa_handle *h) {
+    if (!h) return RFA_ERR_INVALID;
+    hipSetDevice(h->device);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    for (auto e : h->ev_pool) hipEventDestroy(e);
+    hipFree(h->d_window);
+    hipFree(h->d_window_none);
+    hipFree(h->d_twc);
+    hipFree(h->d_twf);
+    hipFree(h->d_ring);
+    hipFree(h->d_ring_tmp);
+    hipFree(h->d_peaks);
+    hipFree(h->d_ema);
+    hipFree(h->d_boxcar);
+    hipFree(h->d_in);
+    hipFree(h->d_rows);
+    if (h->h_pinned) hipHostFree(h->h_pinned);
+    if (h->own_stream) hipStreamDestroy(h->own_stream);
+    delete h;
+    return RFA_OK;
+}
+
+int rfa_get_config(const rfa_handle *h, rfa_config *cfg) {
+    if (!h || !cfg) return RFA_ERR_INVALID;
+    *cfg = h->cfg;
+    return RFA_OK;
+}
+
+const char *rfa_last_error(const rfa_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+int rfa_set_stream(rfa_handle *h, void *stream) {
+    if (!h) return RFA_ERR_INVALID;
+    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    return RFA_OK;
+}
+
+int rfa_get_stream(const rfa_handle *h, void **stream) {
+    if (!h || !stream) return RFA_ERR_INVALID;
+    *stream = (void *)h->stream;
+    return RFA_OK;
+}
+
+int rfa_synchronize(rfa_handle *h) {
+    if (!h) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t stride, float *rows,
+                        const float *window, int fmt) {
+    const int n = h->n;
+    const size_t bps = bytes_per_sample(fmt);
+    if (stride == 0) stride = (size_t)n * bps;
+    if (stride < (size_t)n * bps && n_frames > 1) return fail(h, RFA_ERR_INVALID, "frame stride smaller than a frame");
+    const size_t al = load_alignment(fmt);
+    if ((uintptr_t)in % al || stride % al) return fail(h, RFA_ERR_INVALID, "input pointer/stride misaligned for format");
+    if (n_frames > (size_t)0x7fffffff) return fail(h, RFA_ERR_INVALID, "too many frames");
+    if (n_frames == 0) return RFA_OK;
+    const bool need_state = h->d_peaks || h->d_ema;
+    // state needs the rows of the whole batch: use the caller's, else the ring
+    // when every frame lands there, else a staging buffer
+    float *state_rows = rows;
+    bool rows_in_ring = false;
+    if (need_state && !rows) {
+        if (h->d_ring && n_frames <= (size_t)h->ring_rows) {
+            rows_in_ring = true;
+        } else {
+            int rc = ensure_device_buffer(h, (void **)&h->d_rows, &h->d_rows_cap, n_frames * (size_t)n * sizeof(float));
+            if (rc) return rc;
+            state_rows = h->d_rows;
+        }
+    }
+    FftLaunch a;
+    a.in = (const uint8_t *)in;
+    a.frame_stride = (long long)stride;
+    a.n_frames = (int)n_frames;
+    a.fmt = fmt;
+    a.window = window;
+    a.rows = state_rows;
+    if (h->d_ring) {
+        a.ring = h->d_ring;
+        a.ring_rows = h->ring_rows;
+        a.ring_base = h->write_index;
+        a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
+    }
+    int rc = launch_main(h, a);
+    if (rc) return rc;
+    if (need_state) {
+        rfa::StateLaunch s;
+        s.n = n;
+        s.n_frames = (int)n_frames;
+        s.peaks = h->d_peaks;
+        s.ema = h->d_ema;
+        s.ema_alpha = h->cfg.ema_alpha;
+        s.stream = h->stream;
+        if (rows_in_ring) {
+            // frames occupy ring rows write_index, write_index-1, ... (mod R): walk them in order
+            // with a negative stride when they do not wrap, else frame by frame
+            const int w0 = h->write_index;
+            const int nf = (int)n_frames;
+            if (w0 - (nf - 1) >= 0) {
+                s.rows = h->d_ring + (size_t)w0 * n;
+                s.row_stride = -(long long)n;
+                s.n_frames = nf;
+                HIPCHK(h, rfa::launch_state(s));
+            } else {
+                for (int f = 0; f < nf; f++) {
+                    int rr = ((w0 - f) % h->ring_rows + h->ring_rows) % h->ring_rows;
+                    s.rows = h->d_ring + (size_t)rr * n;
+                    s.row_stride = 0;
+                    s.n_frames = 1;
+                    HIPCHK(h, rfa::launch_state(s));
+                }
+            }
+        } else {
+            s.rows = state_rows;
+            s.row_stride = n;
+            HIPCHK(h, rfa::launch_state(s));
+        }
+    }
+    if (h->d_ring) {
+        const long long R = h->ring_rows;
+        const long long last = (long long)n_frames - 1;
+        h->read_index = (int)((((long long)h->write_index - last) % R + R) % R);
+        h->write_index = h->read_index == 0 ? h->ring_rows - 1 : h->read_index - 1;  // FftProcessor.kt:226-227
+    }
+    h->have_rows = true;
+    if (h->profile) drain_events(h, false);
+    return RFA_OK;
+}
+
+int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows) {
+    if (!h || (!in && n_frames)) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    return process_impl(h, in, n_frames, frame_stride_bytes, rows, h->d_window, h->cfg.input_format);
+}
+
+int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows) {
+    if (!h || (!in && n_frames)) return RFA_ERR_INVALID;
+    if (n_frames == 0) return RFA_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    const size_t bps = bytes_per_sample(h->cfg.input_format);
+    const size_t stride = frame_stride_bytes ? frame_stride_bytes : (size_t)h->n * bps;
+    const size_t in_bytes = (n_frames - 1) * stride + (size_t)h->n * bps;
+    rc = ensure_device_buffer(h, &h->d_in, &h->d_in_cap, in_bytes);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->d_in, in, in_bytes, hipMemcpyHostToDevice, h->stream));
+    float *d_rows = nullptr;
+    if (rows) {
+        rc = ensure_device_buffer(h, (void **)&h->d_rows, &h->d_rows_cap, n_frames * (size_t)h->n * sizeof(float));
+        if (rc) return rc;
+        d_rows = h->d_rows;
+    }
+    rc = process_impl(h, h->d_in, n_frames, stride, d_rows, h->d_window, h->cfg.input_format);
+    if (rc) return rc;
+    if (rows)
+        HIPCHK(h, hipMemcpyAsync(rows, d_rows, n_frames * (size_t)h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
+    if (!h || sample_rate <= 0) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    if (!h->have_tuning) {
+        h->have_tuning = true;
+        h->last_frequency = frequency;
+        h->last_sample_rate = sample_rate;
+        return reset_peaks_ema(h);
+    }
+    const bool fchg = frequency != h->last_frequency;
+    const bool schg = sample_rate != h->last_sample_rate;
+    if (!fchg && !schg) return RFA_OK;
+    const int64_t fdiff = h->last_frequency - frequency;  // FftProcessor.kt:173
+    h->last_frequency = frequency;
+    h->last_sample_rate = sample_rate;
+    if (h->d_ring) {
+        if (fdiff != 0) {
+            // FftProcessor.kt:143,199: (fdiff * (N / sampleRate.toFloat())).toInt(), float arithmetic
+            const float samples_per_hz = (float)h->n / (float)sample_rate;
+            const float prod = (float)fdiff * samples_per_hz;
+            long long off;
+            if (std::isnan(prod)) off = 0;
+            else if (prod >= 2147483647.0f) off = 2147483647LL;
+            else if (prod <= -2147483648.0f) off = -2147483648LL;
+            else off = (long long)prod;  // truncation toward zero
+            if ((off < 0 && -off < h->n) || (off >= 0 && off < h->n)) {
+                HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, (int)off, kRingFill,
+                                                 h->stream));
+                std::swap(h->d_ring, h->d_ring_tmp);
+            } else {
+                rc = clear_ring(h);
+                if (rc) return rc;
+            }
+        } else {
+            rc = clear_ring(h);  // sample-rate change, FftProcessor.kt:216-219
+            if (rc) return rc;
+        }
+    }
+    return reset_peaks_ema(h);  // FftProcessor.kt:238-239 (peaks), EMA likewise
+}
+
+int rfa_get_peaks(rfa_handle *h, float *out) {
+    if (!h || !out) return RFA_ERR_INVALID;
+    if (!h->d_peaks) return fail(h, RFA_ERR_STATE, "peak_hold disabled");
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(out, h->d_peaks, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_get_ema(rfa_handle *h, float *out) {
+    if (!h || !out) return RFA_ERR_INVALID;
+    if (!h->d_ema) return fail(h, RFA_ERR_STATE, "EMA disabled");
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(out, h->d_ema, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out) {
+    if (!h || !out || length < 0) return RFA_ERR_INVALID;
+    if (!h->d_ring) return fail(h, RFA_ERR_STATE, "boxcar needs the ring (ring_rows > 0)");
+    if (length >= h->ring_rows) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIPCHK(h, rfa::launch_boxcar(h->d_ring, h->ring_rows, h->n, h->read_index, length, h->d_boxcar, h->stream));
+    HIPCHK(h, hipMemcpyAsync(out, h->d_boxcar, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_index) {
+    if (!h) return RFA_ERR_INVALID;
+    if (!h->d_ring) return fail(h, RFA_ERR_STATE, "ring disabled");
+    int rc = set_device(h);
+    if (rc) return rc;
+    if (out) {
+        HIPCHK(h, hipMemcpyAsync(out, h->d_ring, (size_t)h->ring_rows * h->n * sizeof(float), hipMemcpyDeviceToHost,
+                                 h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    if (read_index) *read_index = h->read_index;
+    if (write_index) *write_index = h->write_index;
+    return RFA_OK;
+}
+
+int rfa_reset_state(rfa_handle *h) {
+    if (!h) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    h->write_index = h->read_index = 0;
+    h->have_rows = false;
+    h->have_tuning = false;
+    rc = clear_ring(h);
+    if (rc) return rc;
+    rc = reset_peaks_ema(h);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema) {
+    if (!h) return RFA_ERR_INVALID;
+    if (ring) *ring = h->d_ring;
+    if (peaks) *peaks = h->d_peaks;
+    if (ema) *ema = h->d_ema;
+    return RFA_OK;
+}
+
+// One frame through the fused kernel from host arrays, no ring/state side effects.
+static int single_frame(rfa_handle *h, const void *host_in, size_t in_bytes, int fmt, const float *d_window,
+                        float *host_db, float2 *host_cplx) {
+    int rc = set_device(h);
+    if (rc) return rc;
+    const size_t n = (size_t)h->n;
+    const size_t out_bytes = host_cplx ? n * sizeof(float2) : n * sizeof(float);
+    rc = ensure_device_buffer(h, &h->d_in, &h->d_in_cap, in_bytes);
+    if (rc) return rc;
+    rc = ensure_device_buffer(h, (void **)&h->d_rows, &h->d_rows_cap, out_bytes);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->d_in, host_in, in_bytes, hipMemcpyHostToDevice, h->stream));
+    FftLaunch a;
+    a.in = (const uint8_t *)h->d_in;
+    a.frame_stride = (long long)in_bytes;
+    a.n_frames = 1;
+    a.fmt = fmt;
+    a.window = d_window;
+    if (host_cplx) a.complex_out = (float2 *)h->d_rows;
+    else a.rows = h->d_rows;
+    rc = launch_main(h, a);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(host_cplx ? (void *)host_cplx : (void *)host_db, h->d_rows, out_bytes,
+                             hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->profile) drain_events(h, false);
+    return RFA_OK;
+}
+
+int rfa_windowed_fft_mag_planar(rfa_handle *h, const float *re, const float *im, float *mag_out, size_t n) {
+    if (!h || !re || !im || !mag_out) return RFA_ERR_INVALID;
+    if (n != (size_t)h->n) return fail(h, RFA_ERR_SIZE, "array length != fft_size");  // NativeDsp.kt:45-46
+    int rc = ensure_pinned(h, 2 * n * sizeof(float));
+    if (rc) return rc;
+    float *p = (float *)h->h_pinned;
+    std::memcpy(p, re, n * sizeof(float));
+    std::memcpy(p + n, im, n * sizeof(float));
+    // NativeDsp.kt always applies its Blackman window (:48-49,55-58)
+    const float *win = h->d_window;
+    std::vector<float> tmp;
+    if (h->cfg.window != RFA_WINDOW_BLACKMAN) {
+        // the handle was built with another window: apply Blackman through a temporary table
+        static thread_local float *d_black = nullptr;
+        static thread_local int d_black_n = 0;
+        if (d_black_n != h->n) {
+            if (d_black) hipFree(d_black);
+            tmp = make_window(h->n, RFA_WINDOW_BLACKMAN);
+            if (hipMalloc(&d_black, n * sizeof(float)) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "window");
+            HIPCHK(h, hipMemcpy(d_black, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice));
+            d_black_n = h->n;
+        }
+        win = d_black;
+    }
+    return single_frame(h, p, 2 * n * sizeof(float), RFA_IN_F32_PLANAR, win, mag_out, nullptr);
+}
+
+int rfa_fft_logmag_interleaved(rfa_handle *h, const float *in, float *mag_out, size_t n) {
+    if (!h || !in || !mag_out) return RFA_ERR_INVALID;
+    if (n != (size_t)h->n) return fail(h, RFA_ERR_SIZE, "array length != fft_size");
+    return single_frame(h, in, 2 * n * sizeof(float), RFA_IN_F32_INTERLEAVED, h->d_window_none, mag_out, nullptr);
+}
+
+int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n) {
+    if (!h || !in || !out) return RFA_ERR_INVALID;
+    if (n != (size_t)h->n) return fail(h, RFA_ERR_SIZE, "array length != fft_size");
+    return single_frame(h, in, 2 * n * sizeof(float), RFA_IN_F32_INTERLEAVED, h->d_window_none, nullptr, (float2 *)out);
+}
+
+int rfa_set_profiling(rfa_handle *h, int enable) {
+    if (!h) return RFA_ERR_INVALID;
+    if (!enable && h->profile) drain_events(h, true);
+    h->profile = enable != 0;
+    return RFA_OK;
+}
+
+int rfa_get_kernel_time(rfa_handle *h, double *total_ms, int64_t *launches) {
+    if (!h) return RFA_ERR_INVALID;
+    drain_events(h, true);
+    if (total_ms) *total_ms = h->kernel_ms;
+    if (launches) *launches = h->launches;
+    return RFA_OK;
+}
+
+}  // extern "C"

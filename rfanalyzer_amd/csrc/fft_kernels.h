@@ -1,0 +1,59 @@
+// Internal launch interface between the engine (engine.hip) and the gfx950
+// kernels (fft_kernels.hip).  Not part of the public C-ABI (include/rfa.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rfa {
+
+// Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
+// 128 KiB + padding, one workgroup per CU).  Larger N split across
+// workgroups (see DESIGN.md "Large N").
+constexpr int kMaxLogM = 14;
+constexpr int kMaxLogSplit = 3;  // up to 8 workgroups per frame (N <= 2^17) in the fused path
+
+struct FftLaunch {
+    // input: n_frames frames, frame f at in + f*frame_stride bytes
+    const uint8_t *in = nullptr;
+    long long frame_stride = 0;
+    int n_frames = 0;
+    int fmt = 0;   // rfa_input_format
+    int logn = 0;  // N = 1 << logn
+    const float *window = nullptr;  // N floats (device); all ones for RFA_WINDOW_NONE
+    // twiddle table W_N^s = coarse[s >> tw_shift] * fine[s & ((1<<tw_shift)-1)]
+    const float2 *tw_coarse = nullptr;
+    const float2 *tw_fine = nullptr;
+    int tw_shift = 0;
+    // outputs (any may be null)
+    float *rows = nullptr;      // n_frames * N, frame order
+    float *ring = nullptr;      // ring_rows * N
+    int ring_rows = 0;
+    int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
+    int ring_first = 0;         // first frame that is stored into the ring
+    float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    hipStream_t stream = nullptr;
+};
+
+// Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
+hipError_t launch_fft(const FftLaunch &a);
+
+// Sequential EMA / peak-hold over n_frames rows (row f at rows + f*row_stride).
+struct StateLaunch {
+    const float *rows = nullptr;
+    long long row_stride = 0;
+    int n_frames = 0;
+    int n = 0;
+    float *peaks = nullptr;  // may be null
+    float *ema = nullptr;    // may be null; -inf = uninitialised
+    float ema_alpha = 0.f;
+    hipStream_t stream = nullptr;
+};
+hipError_t launch_state(const StateLaunch &a);
+
+// Ring maintenance (FftProcessor.kt:197-220) and boxcar (AnalyzerSurface.kt:710-714).
+hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);
+hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s);
+hipError_t launch_boxcar(const float *ring, int rows, int n, int read_index, int length, float *out, hipStream_t s);
+
+}  // namespace rfa

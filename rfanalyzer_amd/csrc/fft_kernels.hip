@@ -1,0 +1,499 @@
+// gfx950 (MI355X / CDNA4) kernels of the spectrum hot path.
+//
+// One workgroup "slot" owns one M-point sub-FFT (M <= 16384) entirely on chip:
+//   global raw IQ  --(convert: Signed8BitIQConverter.java:48-50 / Unsigned8Bit..:48-50 /
+//                     Signed16BitIQConverter.kt:52-55; window: NativeDsp.kt:55-58)-->
+//   registers --(radix-16 Stockham passes, LDS exchange between passes)-->
+//   registers --(10*log10(sqrt((Re/N)^2+(Im/N)^2)), fft-shift: nativedsp.cpp:72-79)--> rows / ring
+// Each thread holds 16 complex points in VGPRs; one Stockham pass = twiddle +
+// in-register DFT-16 (4x4) + one LDS round trip.  The forward transform has
+// sign -1 and is unscaled, natural output order (pffft.h:117, pffft.c:1660).
+//
+// N > 16384 (N = RS*M, RS in {2,4,8}): RS workgroups share one frame.  Workgroup
+// r computes the decimation-in-frequency residue class X[r + RS*k]: it reads
+// the WHOLE frame, forms y_r[m] = W_N^{m r} * sum_j x[m + jM] W_RS^{j r}, and runs
+// the M-point FFT of y_r.  The RS workgroups of a frame get block ids that are
+// congruent mod 8 so that, under the observed round-robin XCD placement, they
+// share one L2 and the re-reads of the frame hit there (speed only).
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "fft_kernels.h"
+
+namespace rfa {
+
+// ----------------------------------------------------------------- complex helpers
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
+__device__ __forceinline__ float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }  // * (+i)
+
+// exp(-2*pi*i*m/16), correctly rounded fp32 constants.
+constexpr float kC1 = 0.923879532511286756f;  // cos(pi/8)
+constexpr float kS1 = 0.382683432365089772f;  // sin(pi/8)
+constexpr float kR2 = 0.707106781186547524f;  // sqrt(1/2)
+
+// x * W_16^m (m in 0..15), constant-folded per call site.
+template <int m>
+__device__ __forceinline__ float2 w16(float2 x) {
+    constexpr int q = m & 15;
+    if constexpr (q == 0) return x;
+    else if constexpr (q == 4) return mul_mi(x);
+    else if constexpr (q == 8) return make_float2(-x.x, -x.y);
+    else if constexpr (q == 12) return mul_pi(x);
+    else if constexpr (q == 2) return make_float2((x.x + x.y) * kR2, (x.y - x.x) * kR2);
+    else if constexpr (q == 6) return make_float2((x.y - x.x) * kR2, -(x.x + x.y) * kR2);
+    else if constexpr (q == 10) return make_float2(-(x.x + x.y) * kR2, (x.x - x.y) * kR2);
+    else if constexpr (q == 14) return make_float2((x.x - x.y) * kR2, (x.x + x.y) * kR2);
+    else {
+        constexpr float c[16] = {1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1, 0, kS1, kR2, kC1};
+        constexpr float s[16] = {0, kS1, kR2, kC1, 1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1};
+        // W = cos - i sin
+        return cmul(x, make_float2(c[q], -s[q]));
+    }
+}
+
+// In-register forward DFTs, natural order in and out.
+__device__ __forceinline__ void dft2(float2 &a, float2 &b) {
+    float2 t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+__device__ __forceinline__ void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
+    float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
+    x0 = cadd(s02, s13);
+    x2 = csub(s02, s13);
+    x1 = cadd(d02, mul_mi(d13));
+    x3 = cadd(d02, mul_pi(d13));
+}
+
+template <int R>
+__device__ __forceinline__ void dft(float2 *u);
+
+template <>
+__device__ __forceinline__ void dft<2>(float2 *u) { dft2(u[0], u[1]); }
+template <>
+__device__ __forceinline__ void dft<4>(float2 *u) { dft4(u[0], u[1], u[2], u[3]); }
+template <>
+__device__ __forceinline__ void dft<8>(float2 *u) {
+    // t = 2*t1 + t2; DFT-4 over t1, twiddle W_8^{t2 q1} (= W_16^{2 t2 q1}), DFT-2 over t2.
+    dft4(u[0], u[2], u[4], u[6]);
+    dft4(u[1], u[3], u[5], u[7]);
+    u[3] = w16<2>(u[3]);
+    u[5] = w16<4>(u[5]);
+    u[7] = w16<6>(u[7]);
+    dft2(u[0], u[1]);
+    dft2(u[2], u[3]);
+    dft2(u[4], u[5]);
+    dft2(u[6], u[7]);
+    // position 2*q1 + q2 holds Y[q1 + 4 q2]
+    float2 y[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) y[q] = u[2 * (q & 3) + (q >> 2)];
+#pragma unroll
+    for (int q = 0; q < 8; q++) u[q] = y[q];
+}
+template <>
+__device__ __forceinline__ void dft<16>(float2 *u) {
+    // t = 4*t1 + t2; DFT-4 over t1, twiddle W_16^{t2 q1}, DFT-4 over t2.
+    dft4(u[0], u[4], u[8], u[12]);
+    dft4(u[1], u[5], u[9], u[13]);
+    dft4(u[2], u[6], u[10], u[14]);
+    dft4(u[3], u[7], u[11], u[15]);
+    u[5] = w16<1>(u[5]);
+    u[6] = w16<2>(u[6]);
+    u[7] = w16<3>(u[7]);
+    u[9] = w16<2>(u[9]);
+    u[10] = w16<4>(u[10]);
+    u[11] = w16<6>(u[11]);
+    u[13] = w16<3>(u[13]);
+    u[14] = w16<6>(u[14]);
+    u[15] = w16<9>(u[15]);
+    dft4(u[0], u[1], u[2], u[3]);
+    dft4(u[4], u[5], u[6], u[7]);
+    dft4(u[8], u[9], u[10], u[11]);
+    dft4(u[12], u[13], u[14], u[15]);
+    // position 4*q1 + q2 holds Y[q1 + 4 q2]
+    float2 y[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) y[q] = u[4 * (q & 3) + (q >> 2)];
+#pragma unroll
+    for (int q = 0; q < 16; q++) u[q] = y[q];
+}
+
+// ----------------------------------------------------------------- geometry
+template <int LOGM>
+struct Geo {
+    static constexpr int M = 1 << LOGM;
+    static constexpr int TPF = M / 16;                      // threads per sub-FFT, 16 points each
+    static constexpr int SLOTS = TPF >= 256 ? 1 : 256 / TPF;  // sub-FFTs per workgroup
+    static constexpr int THREADS = TPF * SLOTS;
+    static constexpr int PADM = M + M / 8;                  // LDS words (float2) per slot
+    static constexpr int NP16 = LOGM / 4;                   // radix-16 passes
+    static constexpr int LASTR = 1 << (LOGM % 4);           // trailing small radix (1 = none)
+    static constexpr int NPASS = NP16 + (LASTR > 1 ? 1 : 0);
+};
+
+// Padded LDS address: two float2 of padding per 16 keeps the first pass's
+// 16-consecutive-point writes (stride 144 B between lanes) conflict-free.
+__device__ __forceinline__ int pad(int e) { return e + ((e >> 4) << 1); }
+
+template <int Q, int LOGM>
+struct PassInfo {
+    using G = Geo<LOGM>;
+    static constexpr int R = (Q < G::NP16) ? 16 : G::LASTR;
+    static constexpr int PREV_LOG = 4 * (Q < G::NP16 ? Q : G::NP16);
+    static constexpr int P = 1 << PREV_LOG;  // product of earlier radices
+    static constexpr int NB = 16 / R;        // butterflies per thread
+};
+
+// Twiddle W_N^s from the two-level LDS table.
+__device__ __forceinline__ float2 tw(const float2 *twc, const float2 *twf, int s, int shift) {
+    return cmul(twc[s >> shift], twf[s & ((1 << shift) - 1)]);
+}
+
+// Read the inputs of pass Q from LDS into v.
+template <int Q, int LOGM>
+__device__ __forceinline__ void lds_read(float2 (&v)[16], const float2 *buf, int tid) {
+    using PI = PassInfo<Q, LOGM>;
+    using G = Geo<LOGM>;
+#pragma unroll
+    for (int b = 0; b < PI::NB; b++) {
+        const int i = tid + b * G::TPF;
+#pragma unroll
+        for (int t = 0; t < PI::R; t++) v[b * PI::R + t] = buf[pad(i + t * (G::M / PI::R))];
+    }
+}
+
+// Apply the data twiddles of pass Q and its in-register DFTs.
+template <int Q, int LOGM>
+__device__ __forceinline__ void butterflies(float2 (&v)[16], int tid, const float2 *twc, const float2 *twf,
+                                            int shift, int tw_scale) {
+    using PI = PassInfo<Q, LOGM>;
+    using G = Geo<LOGM>;
+#pragma unroll
+    for (int b = 0; b < PI::NB; b++) {
+        const int i = tid + b * G::TPF;
+        if constexpr (PI::P > 1) {
+            const int k = i & (PI::P - 1);
+            // W_{P R}^{t k} = W_N^{t k N/(P R)};  tw_scale = N / M
+            const int base = k * (G::M / (PI::P * PI::R)) * tw_scale;
+#pragma unroll
+            for (int t = 1; t < PI::R; t++) v[b * PI::R + t] = cmul(v[b * PI::R + t], tw(twc, twf, t * base, shift));
+        }
+        dft<PI::R>(&v[b * PI::R]);
+    }
+}
+
+// Write the outputs of pass Q into LDS (Stockham autosort destination).
+template <int Q, int LOGM>
+__device__ __forceinline__ void lds_write(const float2 (&v)[16], float2 *buf, int tid) {
+    using PI = PassInfo<Q, LOGM>;
+    using G = Geo<LOGM>;
+#pragma unroll
+    for (int b = 0; b < PI::NB; b++) {
+        const int i = tid + b * G::TPF;
+        const int k = i & (PI::P - 1);
+        const int j = (i - k) * PI::R + k;
+#pragma unroll
+        for (int t = 0; t < PI::R; t++) buf[pad(j + t * PI::P)] = v[b * PI::R + t];
+    }
+}
+
+template <int Q, int LOGM>
+__device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid, const float2 *twc,
+                                           const float2 *twf, int shift, int tw_scale) {
+    using G = Geo<LOGM>;
+    butterflies<Q, LOGM>(v, tid, twc, twf, shift, tw_scale);
+    if constexpr (Q + 1 < G::NPASS) {
+        lds_write<Q, LOGM>(v, buf, tid);
+        __syncthreads();
+        lds_read<Q + 1, LOGM>(v, buf, tid);
+        __syncthreads();
+        run_passes<Q + 1, LOGM>(v, buf, tid, twc, twf, shift, tw_scale);
+    }
+}
+
+// ----------------------------------------------------------------- input conversion
+// One complex sample s of a frame, converted exactly as the reference LUTs do
+// (all scalings are exact powers of two, so the LUT values are reproduced bit for bit).
+template <int FMT>
+__device__ __forceinline__ float2 load_iq(const uint8_t *fb, int s, int n) {
+    if constexpr (FMT == 0) {  // s8: (b)/128
+        const unsigned v = *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
+        return make_float2((float)(signed char)(v & 0xff) * (1.0f / 128.0f),
+                           (float)(signed char)(v >> 8) * (1.0f / 128.0f));
+    } else if constexpr (FMT == 1) {  // u8: (b - 127.4f)/128
+        const unsigned v = *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
+        return make_float2(((float)(v & 0xff) - 127.4f) * (1.0f / 128.0f),
+                           ((float)(v >> 8) - 127.4f) * (1.0f / 128.0f));
+    } else if constexpr (FMT == 2) {  // s16le: s/32768
+        const unsigned v = *reinterpret_cast<const unsigned *>(fb + 4 * (size_t)s);
+        return make_float2((float)(short)(v & 0xffff) * (1.0f / 32768.0f),
+                           (float)(short)(v >> 16) * (1.0f / 32768.0f));
+    } else if constexpr (FMT == 3) {  // f32 interleaved
+        return *reinterpret_cast<const float2 *>(fb + 8 * (size_t)s);
+    } else {  // f32 planar: re[N] then im[N]
+        const float *f = reinterpret_cast<const float *>(fb);
+        return make_float2(f[s], f[(size_t)n + s]);
+    }
+}
+
+// x * W_R^q for a wave-uniform runtime q (R in {2,4,8}).
+__device__ __forceinline__ float2 rot8(float2 x, int q8) {
+    switch (q8 & 7) {
+    case 0: return x;
+    case 1: return w16<2>(x);
+    case 2: return w16<4>(x);
+    case 3: return w16<6>(x);
+    case 4: return w16<8>(x);
+    case 5: return w16<10>(x);
+    case 6: return w16<12>(x);
+    default: return w16<14>(x);
+    }
+}
+
+// ----------------------------------------------------------------- main kernel
+template <int LOGM, int RS, int FMT, bool COMPLEX_OUT>
+__global__ void __launch_bounds__(Geo<LOGM>::THREADS) fft_rows_kernel(FftLaunch a) {
+    using G = Geo<LOGM>;
+    constexpr int M = G::M;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int n = M * RS;
+    const int shift = a.tw_shift;
+    const int nc = n >> shift, nf = 1 << shift;
+    float2 *twc = lds;
+    float2 *twf = lds + nc;
+    float2 *data = lds + ((nc + nf + 1) & ~1);
+
+    // copy the two-level twiddle table into LDS
+    for (int e = threadIdx.x; e < nc; e += G::THREADS) twc[e] = a.tw_coarse[e];
+    for (int e = threadIdx.x; e < nf; e += G::THREADS) twf[e] = a.tw_fine[e];
+
+    const int slot = threadIdx.x / G::TPF;
+    const int tid = threadIdx.x - slot * G::TPF;
+    float2 *buf = data + slot * G::PADM;
+
+    int frame, r;
+    if constexpr (RS == 1) {
+        frame = blockIdx.x * G::SLOTS + slot;
+        r = 0;
+    } else {
+        // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there
+        const int b = blockIdx.x;
+        const int g = b / (8 * RS), rem = b % (8 * RS);
+        r = rem / 8;
+        frame = g * 8 + (rem & 7);
+    }
+    const bool active = frame < a.n_frames;
+    const uint8_t *fb = a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride;
+    __syncthreads();
+
+    // pass-0 inputs: x[tid + t*TPF], t = 0..15
+    float2 v[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++) {
+        const int m = tid + t * G::TPF;
+        if constexpr (RS == 1) {
+            const float w = a.window[m];
+            const float2 x = load_iq<FMT>(fb, m, n);
+            v[t] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
+        } else {
+            float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < RS; j++) {
+                const int s = m + j * M;
+                const float w = a.window[s];
+                const float2 x = load_iq<FMT>(fb, s, n);
+                const float2 xw = make_float2(x.x * w, x.y * w);
+                acc = cadd(acc, rot8(xw, (j * r * (8 / RS)) & 7));
+            }
+            v[t] = (r == 0) ? acc : cmul(acc, tw(twc, twf, m * r, shift));
+        }
+    }
+
+    run_passes<0, LOGM>(v, buf, tid, twc, twf, shift, RS);
+
+    // last pass outputs: sub-bin i + t*P_last, i = tid + b*TPF
+    using PL = PassInfo<G::NPASS - 1, LOGM>;
+    if (!active) return;
+    if constexpr (COMPLEX_OUT) {
+        float2 *out = a.complex_out + (size_t)frame * n;
+#pragma unroll
+        for (int b = 0; b < PL::NB; b++) {
+#pragma unroll
+            for (int t = 0; t < PL::R; t++) {
+                const int ks = tid + b * G::TPF + t * PL::P;
+                out[r + RS * ks] = v[b * PL::R + t];
+            }
+        }
+    } else {
+        const float inv_n = 1.0f / (float)n;  // exact (power of two)
+        float *row = a.rows ? a.rows + (size_t)frame * n : nullptr;
+        float *ring = nullptr;
+        if (a.ring && frame >= a.ring_first) {
+            int rr = (a.ring_base - frame) % a.ring_rows;
+            if (rr < 0) rr += a.ring_rows;
+            ring = a.ring + (size_t)rr * n;
+        }
+#pragma unroll
+        for (int b = 0; b < PL::NB; b++) {
+#pragma unroll
+            for (int t = 0; t < PL::R; t++) {
+                const int ks = tid + b * G::TPF + t * PL::P;
+                const int kk = r + RS * ks;
+                const int o = (kk + (n >> 1)) & (n - 1);
+                const float2 x = v[b * PL::R + t];
+                const float re = x.x * inv_n, im = x.y * inv_n;
+                const float p = re * re + im * im;  // nativedsp.cpp:73-76
+                const float db = 5.0f * log10f(p);   // == 10*log10(sqrt(p)), nativedsp.cpp:78
+                if (row) row[o] = db;
+                if (ring) ring[o] = db;
+            }
+        }
+    }
+}
+
+// ----------------------------------------------------------------- dispatch
+template <int LOGM, int RS, int FMT, bool CO>
+static hipError_t launch_one(const FftLaunch &a) {
+    using G = Geo<LOGM>;
+    const int n = G::M * RS;
+    const int nc = n >> a.tw_shift, nf = 1 << a.tw_shift;
+    const size_t lds = (size_t)(((nc + nf + 1) & ~1) + G::SLOTS * G::PADM) * sizeof(float2);
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&fft_rows_kernel<LOGM, RS, FMT, CO>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    unsigned blocks;
+    if (RS == 1) blocks = (unsigned)((a.n_frames + G::SLOTS - 1) / G::SLOTS);
+    else blocks = (unsigned)(((a.n_frames + 7) / 8) * 8 * RS);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((fft_rows_kernel<LOGM, RS, FMT, CO>), dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
+    return hipGetLastError();
+}
+
+template <int LOGM, int RS, bool CO>
+static hipError_t by_fmt(const FftLaunch &a) {
+    switch (a.fmt) {
+    case 0: return launch_one<LOGM, RS, 0, CO>(a);
+    case 1: return launch_one<LOGM, RS, 1, CO>(a);
+    case 2: return launch_one<LOGM, RS, 2, CO>(a);
+    case 3: return launch_one<LOGM, RS, 3, CO>(a);
+    case 4: return launch_one<LOGM, RS, 4, CO>(a);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <bool CO>
+static hipError_t by_size(const FftLaunch &a) {
+    switch (a.logn) {
+    case 6: return by_fmt<6, 1, CO>(a);
+    case 7: return by_fmt<7, 1, CO>(a);
+    case 8: return by_fmt<8, 1, CO>(a);
+    case 9: return by_fmt<9, 1, CO>(a);
+    case 10: return by_fmt<10, 1, CO>(a);
+    case 11: return by_fmt<11, 1, CO>(a);
+    case 12: return by_fmt<12, 1, CO>(a);
+    case 13: return by_fmt<13, 1, CO>(a);
+    case 14: return by_fmt<14, 1, CO>(a);
+    case 15: return by_fmt<14, 2, CO>(a);
+    case 16: return by_fmt<14, 4, CO>(a);
+    case 17: return by_fmt<14, 8, CO>(a);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_fft(const FftLaunch &a) {
+    if (a.complex_out) {
+        if (a.fmt != 3) return hipErrorInvalidValue;
+        switch (a.logn) {  // complex output: f32 interleaved only
+#define RFA_CO(L, RS) \
+    case (L + (RS == 1 ? 0 : (RS == 2 ? 1 : (RS == 4 ? 2 : 3)))): return launch_one<L, RS, 3, true>(a);
+            RFA_CO(6, 1) RFA_CO(7, 1) RFA_CO(8, 1) RFA_CO(9, 1) RFA_CO(10, 1) RFA_CO(11, 1) RFA_CO(12, 1)
+            RFA_CO(13, 1) RFA_CO(14, 1) RFA_CO(14, 2) RFA_CO(14, 4) RFA_CO(14, 8)
+#undef RFA_CO
+        default: return hipErrorInvalidValue;
+        }
+    }
+    return by_size<false>(a);
+}
+
+// ----------------------------------------------------------------- state / ring kernels
+// Peak-hold (FftProcessor.kt:241-242) and EMA (extension; GlobalPerformanceData.kt:44-50
+// idiom, -inf/uninitialised state re-seeded by the next frame), frame by frame.
+__global__ void state_kernel(StateLaunch a) {
+    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bin >= a.n) return;
+    float pk = a.peaks ? a.peaks[bin] : 0.f;
+    float em = a.ema ? a.ema[bin] : 0.f;
+    const float al = a.ema_alpha;
+    for (int f = 0; f < a.n_frames; f++) {
+        const float x = a.rows[(size_t)f * a.row_stride + bin];
+        pk = fmaxf(pk, x);
+        em = (em > -INFINITY) ? em + al * (x - em) : x;
+    }
+    if (a.peaks) a.peaks[bin] = pk;
+    if (a.ema) a.ema[bin] = em;
+}
+
+hipError_t launch_state(const StateLaunch &a) {
+    if (a.n_frames <= 0) return hipSuccess;
+    const int tpb = 256;
+    hipLaunchKernelGGL(state_kernel, dim3((a.n + tpb - 1) / tpb), dim3(tpb), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+__global__ void fill_kernel(float *p, long long count, float value) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+         i += (long long)gridDim.x * blockDim.x)
+        p[i] = value;
+}
+
+hipError_t launch_fill(float *p, long long count, float value, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    long long blocks = (count + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p, count, value);
+    return hipGetLastError();
+}
+
+// dst[row][i] = src[row][i - shift] (fill outside) -- FftProcessor.kt:202-209
+__global__ void ring_shift_kernel(const float *src, float *dst, int n, int shift, float fill) {
+    const int row = blockIdx.y;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int s = i - shift;
+        dst[(size_t)row * n + i] = (s >= 0 && s < n) ? src[(size_t)row * n + s] : fill;
+    }
+}
+
+hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    int bx = (n + 255) / 256;
+    if (bx > 64) bx = 64;
+    hipLaunchKernelGGL(ring_shift_kernel, dim3(bx, rows), dim3(256), 0, s, src, dst, n, shift, fill);
+    return hipGetLastError();
+}
+
+// AnalyzerSurface.kt:710-714 at bin resolution: fp32 sum newest-first, / (L+1).
+__global__ void boxcar_kernel(const float *ring, int rows, int n, int read_index, int length, float *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float acc = 0.f;
+    for (int r = 0; r <= length; r++) acc += ring[(size_t)((read_index + r) % rows) * n + i];
+    out[i] = acc / (float)(length + 1);
+}
+
+hipError_t launch_boxcar(const float *ring, int rows, int n, int read_index, int length, float *out,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(boxcar_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ring, rows, n, read_index, length, out);
+    return hipGetLastError();
+}
+
+}  // namespace rfa

@@ -1,0 +1,182 @@
+"""SpectrumEngine: Python face of one librfa handle.
+
+One engine = one reference ``FftProcessor`` + ``NativeDsp`` pair
+(analyzer/FftProcessor.kt:64-257, nativedsp/.../NativeDsp.kt) living on one
+GPU: raw IQ frames in, waterfall rows out, with the ring, peak-hold and
+averaging state kept in HBM.  All compute runs in librfa's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import AVG_MODES, BYTES_PER_SAMPLE, FORMATS, WINDOWS, RfaConfig, check
+
+_fp = ctypes.POINTER(ctypes.c_float)
+
+
+def _fptr(a: np.ndarray):
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_fp)
+
+
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        return np.ascontiguousarray(data).reshape(-1).view(np.uint8)
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+class SpectrumEngine:
+    def __init__(self, fft_size: int, window: str = "blackman", input_format: str = "s8", avg: str = "none",
+                 avg_length: int = 0, ema_alpha: float = 0.1, peak_hold: bool = False, ring_rows: int = 400,
+                 device: int = 0):
+        cfg = RfaConfig()
+        _lib.lib().rfa_default_config(ctypes.byref(cfg))
+        cfg.fft_size = fft_size
+        cfg.window = WINDOWS[window] if isinstance(window, str) else int(window)
+        cfg.input_format = FORMATS[input_format] if isinstance(input_format, str) else int(input_format)
+        cfg.avg_mode = AVG_MODES[avg] if isinstance(avg, str) else int(avg)
+        cfg.avg_length = avg_length
+        cfg.ema_alpha = ema_alpha
+        cfg.peak_hold = 1 if peak_hold else 0
+        cfg.ring_rows = ring_rows
+        cfg.device_id = device
+        self.cfg = cfg
+        self.n = fft_size
+        self.fmt = cfg.input_format
+        self.bps = BYTES_PER_SAMPLE[self.fmt]
+        h = ctypes.c_void_p()
+        check(_lib.lib().rfa_create(ctypes.byref(cfg), ctypes.byref(h)), "rfa_create")
+        self._h = h
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().rfa_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _check(self, status: int, where: str) -> None:
+        check(status, where, self._h)
+
+    # -- processing -------------------------------------------------------------
+    def frames_in(self, n_bytes: int, frame_stride: int = 0) -> int:
+        fb = self.n * self.bps
+        stride = frame_stride or fb
+        return 0 if n_bytes < fb else (n_bytes - fb) // stride + 1
+
+    def process(self, data, n_frames: int | None = None, frame_stride: int = 0, rows: bool = True):
+        """Host bytes/ndarray in -> (n_frames, N) float32 rows (or None)."""
+        buf = _as_u8(data)
+        if n_frames is None:
+            n_frames = self.frames_in(buf.size, frame_stride)
+        stride = frame_stride or self.n * self.bps
+        need = (n_frames - 1) * stride + self.n * self.bps if n_frames else 0
+        if buf.size < need:
+            raise ValueError(f"input has {buf.size} bytes, {need} needed for {n_frames} frames")
+        out = np.empty((n_frames, self.n), np.float32) if rows else None
+        self._check(_lib.lib().rfa_process_host(self._h, buf.ctypes.data, n_frames, frame_stride,
+                                                out.ctypes.data if rows else None), "rfa_process_host")
+        return out
+
+    def process_device(self, in_ptr: int, n_frames: int, frame_stride: int = 0, rows_ptr: int | None = None) -> None:
+        """Device pointers (e.g. torch .data_ptr()); asynchronous on the engine stream."""
+        self._check(_lib.lib().rfa_process(self._h, in_ptr, n_frames, frame_stride, rows_ptr), "rfa_process")
+
+    def process_tensor(self, t, n_frames: int | None = None, frame_stride: int = 0, rows=None) -> None:
+        """torch.cuda tensors (uint8/int8/float32 input, float32 rows)."""
+        nbytes = t.numel() * t.element_size()
+        if n_frames is None:
+            n_frames = self.frames_in(nbytes, frame_stride)
+        self.process_device(t.data_ptr(), n_frames, frame_stride, rows.data_ptr() if rows is not None else None)
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        self._check(_lib.lib().rfa_set_stream(self._h, stream_ptr), "rfa_set_stream")
+
+    def synchronize(self) -> None:
+        self._check(_lib.lib().rfa_synchronize(self._h), "rfa_synchronize")
+
+    # -- FftProcessor state -----------------------------------------------------
+    def set_tuning(self, frequency: int, sample_rate: int) -> None:
+        self._check(_lib.lib().rfa_set_tuning(self._h, int(frequency), int(sample_rate)), "rfa_set_tuning")
+
+    def peaks(self) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        self._check(_lib.lib().rfa_get_peaks(self._h, _fptr(out)), "rfa_get_peaks")
+        return out
+
+    def ema(self) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        self._check(_lib.lib().rfa_get_ema(self._h, _fptr(out)), "rfa_get_ema")
+        return out
+
+    def boxcar(self, length: int | None = None) -> np.ndarray:
+        out = np.empty(self.n, np.float32)
+        length = self.cfg.avg_length if length is None else length
+        self._check(_lib.lib().rfa_get_boxcar(self._h, length, _fptr(out)), "rfa_get_boxcar")
+        return out
+
+    def ring(self):
+        out = np.empty((self.cfg.ring_rows, self.n), np.float32)
+        ri, wi = ctypes.c_int32(), ctypes.c_int32()
+        self._check(_lib.lib().rfa_get_ring(self._h, _fptr(out), ctypes.byref(ri), ctypes.byref(wi)),
+                    "rfa_get_ring")
+        return out, ri.value, wi.value
+
+    def reset_state(self) -> None:
+        self._check(_lib.lib().rfa_reset_state(self._h), "rfa_reset_state")
+
+    # -- reference seams (host arrays) ------------------------------------------
+    def windowed_fft_mag(self, re: np.ndarray, im: np.ndarray, mag_out: np.ndarray) -> bool:
+        """NativeDsp.performWindowedFftAndReturnMag (NativeDsp.kt:43-62)."""
+        re = np.ascontiguousarray(re, np.float32)
+        im = np.ascontiguousarray(im, np.float32)
+        if im.size != re.size or mag_out.size != re.size:
+            return False
+        rc = _lib.lib().rfa_windowed_fft_mag_planar(self._h, _fptr(re), _fptr(im), _fptr(mag_out), re.size)
+        if rc == _lib.RFA_ERR_SIZE:
+            return False
+        self._check(rc, "rfa_windowed_fft_mag_planar")
+        return True
+
+    def fft_logmag(self, interleaved: np.ndarray) -> np.ndarray:
+        """JNI performFFTAndLogMag (nativedsp.cpp:44-81)."""
+        x = np.ascontiguousarray(interleaved, np.float32)
+        out = np.empty(x.size // 2, np.float32)
+        self._check(_lib.lib().rfa_fft_logmag_interleaved(self._h, _fptr(x), _fptr(out), out.size),
+                    "rfa_fft_logmag_interleaved")
+        return out
+
+    def fft_ordered(self, interleaved: np.ndarray) -> np.ndarray:
+        """JNI performFFT (nativedsp.cpp:19-42)."""
+        x = np.ascontiguousarray(interleaved, np.float32)
+        out = np.empty_like(x)
+        self._check(_lib.lib().rfa_fft_ordered(self._h, _fptr(x), _fptr(out), x.size // 2), "rfa_fft_ordered")
+        return out
+
+    # -- profiling --------------------------------------------------------------
+    def set_profiling(self, on: bool) -> None:
+        self._check(_lib.lib().rfa_set_profiling(self._h, 1 if on else 0), "rfa_set_profiling")
+
+    def kernel_time(self):
+        ms, n = ctypes.c_double(), ctypes.c_int64()
+        self._check(_lib.lib().rfa_get_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)),
+                    "rfa_get_kernel_time")
+        return ms.value, n.value

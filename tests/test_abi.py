@@ -1,0 +1,92 @@
+"""CPU: the C-ABI library builds, loads without a GPU and exports every symbol
+the public headers declare; device-less behaviour is a clean status code."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def declared_symbols():
+    names = set()
+    for fn in os.listdir(INCLUDE):
+        if not fn.endswith(".h"):
+            continue
+        text = open(os.path.join(INCLUDE, fn)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names |= set(re.findall(r"\b(rfa_[a-z_]+)\s*\(", text))
+        names |= set(re.findall(r"\b(Java_com_mantz_1it_nativedsp_NativeDsp_\w+)\s*\(", text))
+    return sorted(names)
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import rfanalyzer_amd
+    rfanalyzer_amd.build()
+    return rfanalyzer_amd.lib()
+
+
+def test_headers_declare_expected_surface():
+    syms = declared_symbols()
+    for must in ["rfa_create", "rfa_process", "rfa_process_host", "rfa_set_tuning", "rfa_get_peaks",
+                 "rfa_get_boxcar", "rfa_get_ema", "rfa_windowed_fft_mag_planar",
+                 "Java_com_mantz_1it_nativedsp_NativeDsp_performFFT",
+                 "Java_com_mantz_1it_nativedsp_NativeDsp_performFFTAndLogMag"]:
+        assert must in syms
+
+
+def test_every_declared_symbol_is_exported(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib._name], capture_output=True, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if line.strip())
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    for s in declared_symbols():
+        assert getattr(lib, s) is not None
+
+
+def test_library_embeds_gfx950_code_object(lib):
+    data = open(lib._name, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_status_strings_and_defaults(lib):
+    from rfanalyzer_amd._lib import RfaConfig
+    assert lib.rfa_abi_version() == 1
+    assert lib.rfa_status_string(0) == b"ok"
+    assert lib.rfa_status_string(-2) == b"size mismatch"
+    c = RfaConfig()
+    lib.rfa_default_config(ctypes.byref(c))
+    assert (c.fft_size, c.window, c.input_format, c.ring_rows, c.peak_hold) == (16384, 0, 0, 400, 0)
+
+
+def test_create_without_device_or_with_bad_config(lib):
+    import torch
+
+    from rfanalyzer_amd._lib import RfaConfig
+    c = RfaConfig()
+    lib.rfa_default_config(ctypes.byref(c))
+    h = ctypes.c_void_p()
+    c.fft_size = 1000
+    assert lib.rfa_create(ctypes.byref(c), ctypes.byref(h)) == -3  # unsupported size, checked first
+    c.fft_size = 1024
+    c.window = 9
+    assert lib.rfa_create(ctypes.byref(c), ctypes.byref(h)) == -1
+    c.window = 0
+    rc = lib.rfa_create(ctypes.byref(c), ctypes.byref(h))
+    if not torch.cuda.is_available():
+        assert rc == -4 and not h.value  # RFA_ERR_NODEVICE, nothing leaked
+    elif rc == 0:
+        lib.rfa_destroy(h)
+    assert lib.rfa_process(None, None, 0, 0, None) == -1
+    assert lib.rfa_destroy(None) == -1
+
+
+def test_jni_table_layout_constants():
+    text = open(os.path.join(ROOT, "rfanalyzer_amd", "csrc", "jni_min.h")).read()
+    # the compiled static_asserts pin these; make sure they stay in the header
+    for slot in ("171", "200", "205", "213", "228"):
+        assert f"== {slot} * sizeof(void *)" in text

@@ -1,0 +1,127 @@
+"""GPU parity: librfa (HIP, gfx950) vs the reference pffft golden rows and the
+float64 oracle.  Tolerance: 0.01 dB (north star), identical argmax bins."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+import oracle
+import signals
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = gu.manifest()
+FIXTURES = MANIFEST["fixtures"]
+
+
+def _engine(rfa, n, fmt, window, **kw):
+    return rfa.SpectrumEngine(n, window, fmt, **kw)
+
+
+@pytest.mark.parametrize("spec", FIXTURES, ids=[s["name"] for s in FIXTURES])
+def test_rows_match_reference_pffft_and_oracle(rfa, spec):
+    data = gu.fixture_input(spec)
+    with _engine(rfa, spec["n"], spec["fmt"], spec["window"], ring_rows=0) as e:
+        rows = e.process(data, spec["n_frames"], spec.get("packet_size", 0))
+    exp = gu.expected(spec)
+    assert gu.db_diff(rows[:, ::spec["subset_stride"]], exp) <= gu.DB_TOL
+    assert [int(a) for a in np.argmax(rows, axis=1)] == spec["argmax"]
+    ref64 = oracle.spectrum_rows(data, signals.FORMATS[spec["fmt"]], spec["n"], spec["n_frames"],
+                                 spec.get("packet_size"), gu.WINDOW_IDS[spec["window"]])
+    assert gu.db_diff(rows, ref64) <= gu.DB_TOL
+
+
+@pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072])
+@pytest.mark.parametrize("fmt", ["s8", "u8", "s16", "f32", "f32p"])
+def test_all_sizes_and_formats_vs_oracle(rfa, n, fmt):
+    frames = 3 if n <= 16384 else 1
+    data = signals.frames_bytes(n, frames, fmt, seed=n + len(fmt), tones=((0.173, 0.5), (-0.29, 0.01)), noise=0.03)
+    with _engine(rfa, n, fmt, "blackman", ring_rows=0) as e:
+        rows = e.process(data, frames)
+    ref = oracle.spectrum_rows(data, signals.FORMATS[fmt], n, frames, None, oracle.WIN_BLACKMAN)
+    assert gu.db_diff(rows, ref) <= gu.DB_TOL
+    np.testing.assert_array_equal(np.argmax(rows, 1), np.argmax(ref, 1))
+
+
+def test_hann_config2_signal(rfa):
+    """Config 2: 20 Msps cf32, N=16384, Hann (oracle = float64 restatement)."""
+    n, b = 16384, 64
+    data = signals.frames_bytes(n, b, "f32", 2, tones=((1000 / n, 0.5), (5000.5 / n, 0.05)), noise=0.01)
+    with _engine(rfa, n, "f32", "hann", ring_rows=0) as e:
+        rows = e.process(data, b)
+    ref = oracle.spectrum_rows(data, oracle.IN_F32_INTERLEAVED, n, b, None, oracle.WIN_HANN)
+    assert gu.db_diff(rows, ref) <= gu.DB_TOL
+
+
+def test_frame_stride_matches_packet_framing(rfa):
+    """Scheduler framing: frames at packet stride, rest of each packet dropped."""
+    spec = next(s for s in FIXTURES if s["name"] == "file_s8_2msps_n1024")
+    data = gu.fixture_input(spec)
+    with _engine(rfa, 1024, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(data, None, spec["packet_size"])
+    assert rows.shape == (15, 1024)
+    assert gu.db_diff(rows, gu.expected(spec)) <= gu.DB_TOL
+
+
+def test_batch_equals_single_frames_bit_exact(rfa):
+    n, b = 4096, 10
+    data = signals.frames_bytes(n, b, "s8", 9, noise=0.1)
+    with _engine(rfa, n, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(data, b)
+        singles = np.stack([e.process(data[f * 2 * n:(f + 1) * 2 * n], 1)[0] for f in range(b)])
+        again = e.process(data, b)
+    np.testing.assert_array_equal(rows, singles)
+    np.testing.assert_array_equal(rows, again)  # deterministic
+
+
+@pytest.mark.parametrize("n", [1024, 65536])
+def test_scaling_property_plus_3db(rfa, n):
+    """Size-independent property: x2 in f32 is exact through the FFT -> +10*log10(2) dB."""
+    x = np.frombuffer(signals.frames_bytes(n, 2, "f32", 5, noise=0.2), np.float32)
+    with _engine(rfa, n, "f32", "blackman", ring_rows=0) as e:
+        a = e.process(x, 2)
+        b = e.process(x * np.float32(2), 2)
+    np.testing.assert_allclose(b - a, 10 * np.log10(2), atol=2e-5)
+
+
+def test_all_zero_input_gives_minus_inf(rfa):
+    with _engine(rfa, 1024, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(bytes(2 * 1024 * 3), 3)
+    assert np.all(np.isneginf(rows))
+
+
+def test_size_mismatch_and_bad_args(rfa):
+    from rfanalyzer_amd import RfaError
+    with _engine(rfa, 1024, "f32p", "blackman", ring_rows=0) as e:
+        out = np.empty(1024, np.float32)
+        assert not e.windowed_fft_mag(np.zeros(1024, np.float32), np.zeros(512, np.float32), out)
+        assert not e.windowed_fft_mag(np.zeros(512, np.float32), np.zeros(512, np.float32), np.empty(512, np.float32))
+        assert e.process(b"", 0).shape == (0, 1024)
+    with pytest.raises(RfaError):
+        rfa.SpectrumEngine(1000)  # not a power of two
+    with pytest.raises(RfaError):
+        rfa.SpectrumEngine(1 << 21)
+
+
+def test_reference_seams_match_pffft(rfa):
+    if not oracle.ref_available():
+        pytest.skip("reference pffft build absent")
+    n = 16384
+    rng = np.random.default_rng(1)
+    re = rng.standard_normal(n).astype(np.float32)
+    im = rng.standard_normal(n).astype(np.float32)
+    w = oracle.window(n, oracle.WIN_BLACKMAN)
+    inter = oracle.windowed_interleaved(re, im, w)
+    from rfanalyzer_amd.nativedsp import NativeDsp
+    dsp = NativeDsp()
+    mag = np.empty(n, np.float32)
+    assert dsp.performWindowedFftAndReturnMag(re, im, mag)
+    assert gu.db_diff(mag, oracle.ref_fft_logmag(inter)) <= gu.DB_TOL
+    out = np.empty(n, np.float32)
+    dsp.performFFTAndLogMag(inter, out)
+    assert gu.db_diff(out, oracle.ref_fft_logmag(inter)) <= gu.DB_TOL
+    cx = np.empty(2 * n, np.float32)
+    dsp.performFFT(inter, cx)
+    ref = oracle.ref_fft_ordered(inter)
+    err = np.abs((cx[0::2] + 1j * cx[1::2]) - (ref[0::2] + 1j * ref[1::2])).max()
+    assert err / np.abs(ref).max() < 1e-5
+    dsp.close()

@@ -1,0 +1,105 @@
+"""GPU: waterfall ring, retune shift, peak-hold, boxcar and EMA vs the numpy
+restatement of FftProcessor.kt (oracle/processor.py) and the stored sequence."""
+import numpy as np
+import pytest
+
+import golden_util as gu
+import oracle
+from oracle import processor
+
+pytestmark = pytest.mark.gpu
+
+MANIFEST = gu.manifest()
+
+
+def _gpu_sequence(rfa, spec, data, batch):
+    n, nf = spec["n"], spec["n_frames"]
+    e = rfa.SpectrumEngine(n, spec["window"], spec["fmt"], avg="ema", avg_length=spec["boxcar_length"],
+                           ema_alpha=spec["ema_alpha"], peak_hold=True, ring_rows=spec["ring_rows"])
+    f = 0
+    while f < nf:
+        freq, sr = [t for t in spec["tuning"] if t[0] <= f][-1][1:]
+        nxt = min([t[0] for t in spec["tuning"] if t[0] > f] + [nf, f + batch])
+        e.set_tuning(freq, sr)
+        e.process(data[f * 2 * n:nxt * 2 * n], nxt - f, rows=False)
+        f = nxt
+    return e
+
+
+@pytest.mark.parametrize("batch", [1, 7, 40])
+def test_state_sequence_vs_reference(rfa, batch):
+    spec = MANIFEST["state"]
+    data = gu.fixture_input(spec)
+    exp = gu.expected(spec)
+    e = _gpu_sequence(rfa, spec, data, batch)
+    assert gu.db_diff(e.peaks(), exp["peaks"]) <= gu.DB_TOL
+    assert gu.db_diff(e.boxcar(spec["boxcar_length"]), exp["boxcar"]) <= gu.DB_TOL
+    assert gu.db_diff(e.ema(), exp["ema"]) <= gu.DB_TOL
+    ring, ri, wi = e.ring()
+    newest = np.stack([ring[(ri + r) % ring.shape[0]] for r in range(8)])
+    # rows beyond the retune are -9999 fill in both
+    for g, x in zip(newest, exp["ring_newest8"]):
+        fill = x == -9999
+        np.testing.assert_array_equal(g[fill], x[fill])
+        if (~fill).any():
+            assert gu.db_diff(g[~fill], x[~fill]) <= gu.DB_TOL
+    e.close()
+
+
+def test_ring_indices_and_rows_match_processor_restatement(rfa):
+    n, rows_r = 256, 5
+    data = np.random.default_rng(3).integers(-128, 128, size=2 * n * 13, dtype=np.int8).tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, 13, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(n, rows_r, peak_hold=True)
+    e = rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=rows_r)
+    e.set_tuning(100, 1000)
+    for chunk in ([0, 3], [3, 4], [4, 13]):  # batches larger than the ring too
+        got = e.process(data[chunk[0] * 2 * n:chunk[1] * 2 * n], chunk[1] - chunk[0])
+        assert gu.db_diff(got, ref_rows[chunk[0]:chunk[1]]) <= gu.DB_TOL
+        for f in range(*chunk):
+            p.push(ref_rows[f], 100, 1000)
+        ring, ri, wi = e.ring()
+        assert (ri, wi) == (p.read_index, p.write_index)
+        for r in range(rows_r):
+            if np.all(p.ring[r] == -9999):
+                assert np.all(ring[r] == -9999)
+            else:
+                assert gu.db_diff(ring[r], p.ring[r]) <= gu.DB_TOL
+    assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL
+    e.close()
+
+
+@pytest.mark.parametrize("new_freq,new_sr", [(100 + 37, 1000), (100 - 300, 1000), (100 + 999, 1000), (100, 2000)])
+def test_retune_shift_and_clear(rfa, new_freq, new_sr):
+    n, rows_r = 256, 4
+    data = np.random.default_rng(4).integers(-128, 128, size=2 * n * 3, dtype=np.int8).tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, 3, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(n, rows_r, peak_hold=True)
+    e = rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=rows_r)
+    e.set_tuning(100, 1000)
+    e.process(data[: 2 * 2 * n], 2, rows=False)
+    p.push(ref_rows[0], 100, 1000)
+    p.push(ref_rows[1], 100, 1000)
+    e.set_tuning(new_freq, new_sr)
+    e.process(data[2 * 2 * n:], 1, rows=False)
+    p.push(ref_rows[2], new_freq, new_sr)
+    ring, ri, wi = e.ring()
+    assert (ri, wi) == (p.read_index, p.write_index)
+    for r in range(rows_r):
+        fill = p.ring[r] == -9999
+        np.testing.assert_array_equal(ring[r][fill], p.ring[r][fill])
+        if (~fill).any():
+            assert gu.db_diff(ring[r][~fill], p.ring[r][~fill]) <= gu.DB_TOL
+    assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL  # peaks reset on retune
+    e.close()
+
+
+def test_ema_matches_sequential_extension(rfa):
+    n, b = 4096, 50
+    data = np.random.default_rng(5).integers(-128, 128, size=2 * n * b, dtype=np.int8).tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, b, None, oracle.WIN_BLACKMAN)
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.2, ring_rows=0) as e:
+        e.process(data[: 2 * n * 20], 20, rows=False)
+        e.process(data[2 * n * 20:], b - 20, rows=False)
+        got = e.ema()
+    assert gu.db_diff(got, processor.ema_batch(ref_rows, 0.2)) <= gu.DB_TOL
