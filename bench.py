@@ -138,7 +138,8 @@ def main():
     eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
                                         ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
                                         ring_rows=args.ring_rows, device=local)
-    stream = torch.cuda.current_stream(device)
+    stream = torch.cuda.Stream(device)  # a real stream shared by torch and librfa (not the null stream)
+    torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
     pool = make_pool(torch, n, frames, fmt, args.pool_mib, 3 + rank, device)
     eng.set_tuning(100_000_000, 20_000_000)

@@ -103,8 +103,11 @@ RFA_API int rfa_destroy(rfa_handle *h);
 RFA_API int rfa_get_config(const rfa_handle *h, rfa_config *cfg);
 RFA_API const char *rfa_last_error(const rfa_handle *h);
 
-/* Stream control: `stream` is a hipStream_t (NULL = the handle's own stream). */
+/* Stream control: work is enqueued on exactly `stream` (a hipStream_t; NULL is
+ * the HIP null stream) until rfa_use_own_stream() restores the handle's own
+ * non-blocking stream. */
 RFA_API int rfa_set_stream(rfa_handle *h, void *stream);
+RFA_API int rfa_use_own_stream(rfa_handle *h);
 RFA_API int rfa_get_stream(const rfa_handle *h, void **stream);
 RFA_API int rfa_synchronize(rfa_handle *h);
 

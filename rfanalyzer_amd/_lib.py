@@ -79,6 +79,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_last_error": (ctypes.c_char_p, [_h]),
         "rfa_set_stream": (ctypes.c_int, [_h, _vp]),
         "rfa_get_stream": (ctypes.c_int, [_h, ctypes.POINTER(_vp)]),
+        "rfa_use_own_stream": (ctypes.c_int, [_h]),
         "rfa_synchronize": (ctypes.c_int, [_h]),
         "rfa_process": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_process_host": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),

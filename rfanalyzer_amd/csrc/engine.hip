@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -27,7 +28,10 @@ struct rfa_handle {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     float *d_window = nullptr;
-    float *d_window_none = nullptr;  // all ones (already-windowed seams)
+    float *d_window_none = nullptr;   // all ones (already-windowed f32 seams)
+    float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
+    int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
+    int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
@@ -178,6 +182,8 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_coarse = h->d_twc;
     a.tw_fine = h->d_twf;
     a.tw_shift = h->tw_shift;
+    a.diag = h->diag;
+    a.max_logm = h->max_logm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->profile) {
         if (h->ev_pending.size() > 256) drain_events(h, true);
@@ -278,13 +284,21 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     h->stream = h->own_stream;
 
     const int n = h->n;
-    // window tables
-    std::vector<float> w = make_window(n, cfg->window), ones(n, 1.0f);
-    if (hipMalloc(&h->d_window, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
-    if (hipMalloc(&h->d_window_none, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
-    if (hipMemcpy(h->d_window, w.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
-    if (hipMemcpy(h->d_window_none, ones.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
-        return bail(RFA_ERR_HIP);
+    // window tables; the converter's power-of-two scale (1/128 for 8-bit,
+    // 1/32768 for 16-bit) is folded in exactly (scaling commutes with rounding)
+    std::vector<float> w = make_window(n, cfg->window), ones(n, 1.0f), black = make_window(n, RFA_WINDOW_BLACKMAN);
+    const float scale = (cfg->input_format == RFA_IN_S8 || cfg->input_format == RFA_IN_U8) ? 1.0f / 128.0f
+                        : cfg->input_format == RFA_IN_S16LE                                ? 1.0f / 32768.0f
+                                                                                           : 1.0f;
+    for (float &x : w) x *= scale;
+    float **tabs[3] = {&h->d_window, &h->d_window_none, &h->d_window_black};
+    const float *src[3] = {w.data(), ones.data(), black.data()};
+    for (int i = 0; i < 3; i++) {
+        if (hipMalloc(tabs[i], n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMemcpy(*tabs[i], src[i], n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
+    }
+    if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
+    if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
     h->tw_shift = (logn + 1) / 2;
@@ -325,6 +339,7 @@ int rfa_destroy(rfa_handle *h) {
     for (auto e : h->ev_pool) hipEventDestroy(e);
     hipFree(h->d_window);
     hipFree(h->d_window_none);
+    hipFree(h->d_window_black);
     hipFree(h->d_twc);
     hipFree(h->d_twf);
     hipFree(h->d_ring);
@@ -350,7 +365,13 @@ const char *rfa_last_error(const rfa_handle *h) { return h ? h->err.c_str() : "n
 
 int rfa_set_stream(rfa_handle *h, void *stream) {
     if (!h) return RFA_ERR_INVALID;
-    h->stream = stream ? (hipStream_t)stream : h->own_stream;
+    h->stream = (hipStream_t)stream;
+    return RFA_OK;
+}
+
+int rfa_use_own_stream(rfa_handle *h) {
+    if (!h) return RFA_ERR_INVALID;
+    h->stream = h->own_stream;
     return RFA_OK;
 }
 
@@ -416,24 +437,10 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         s.ema_alpha = h->cfg.ema_alpha;
         s.stream = h->stream;
         if (rows_in_ring) {
-            // frames occupy ring rows write_index, write_index-1, ... (mod R): walk them in order
-            // with a negative stride when they do not wrap, else frame by frame
-            const int w0 = h->write_index;
-            const int nf = (int)n_frames;
-            if (w0 - (nf - 1) >= 0) {
-                s.rows = h->d_ring + (size_t)w0 * n;
-                s.row_stride = -(long long)n;
-                s.n_frames = nf;
-                HIPCHK(h, rfa::launch_state(s));
-            } else {
-                for (int f = 0; f < nf; f++) {
-                    int rr = ((w0 - f) % h->ring_rows + h->ring_rows) % h->ring_rows;
-                    s.rows = h->d_ring + (size_t)rr * n;
-                    s.row_stride = 0;
-                    s.n_frames = 1;
-                    HIPCHK(h, rfa::launch_state(s));
-                }
-            }
+            s.rows = h->d_ring;
+            s.ring_rows = h->ring_rows;
+            s.ring_base = h->write_index;
+            HIPCHK(h, rfa::launch_state(s));
         } else {
             s.rows = state_rows;
             s.row_stride = n;
@@ -633,21 +640,7 @@ int rfa_windowed_fft_mag_planar(rfa_handle *h, const float *re, const float *im,
     std::memcpy(p, re, n * sizeof(float));
     std::memcpy(p + n, im, n * sizeof(float));
     // NativeDsp.kt always applies its Blackman window (:48-49,55-58)
-    const float *win = h->d_window;
-    std::vector<float> tmp;
-    if (h->cfg.window != RFA_WINDOW_BLACKMAN) {
-        // the handle was built with another window: apply Blackman through a temporary table
-        static thread_local float *d_black = nullptr;
-        static thread_local int d_black_n = 0;
-        if (d_black_n != h->n) {
-            if (d_black) hipFree(d_black);
-            tmp = make_window(h->n, RFA_WINDOW_BLACKMAN);
-            if (hipMalloc(&d_black, n * sizeof(float)) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "window");
-            HIPCHK(h, hipMemcpy(d_black, tmp.data(), n * sizeof(float), hipMemcpyHostToDevice));
-            d_black_n = h->n;
-        }
-        win = d_black;
-    }
+    const float *win = h->d_window_black;
     return single_frame(h, p, 2 * n * sizeof(float), RFA_IN_F32_PLANAR, win, mag_out, nullptr);
 }
 

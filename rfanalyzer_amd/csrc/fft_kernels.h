@@ -32,16 +32,22 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    int max_logm = 14;  // largest sub-FFT per workgroup (13 = experiment: 2 workgroups per CU)
+    int diag = 0;  // ablation variant (profiling only): 1 no loads, 2 no stores, 4 no FFT passes
     hipStream_t stream = nullptr;
 };
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
 hipError_t launch_fft(const FftLaunch &a);
 
-// Sequential EMA / peak-hold over n_frames rows (row f at rows + f*row_stride).
+// Sequential EMA / peak-hold over n_frames rows.  Row f is at
+// rows + f*row_stride, or, when ring_rows > 0, at rows + ((ring_base - f) mod ring_rows)*n
+// (the reference's reverse-ordered ring, FftProcessor.kt:222-227).
 struct StateLaunch {
     const float *rows = nullptr;
     long long row_stride = 0;
+    int ring_rows = 0;
+    int ring_base = 0;
     int n_frames = 0;
     int n = 0;
     float *peaks = nullptr;  // may be null

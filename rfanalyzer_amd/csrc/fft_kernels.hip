@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <algorithm>
+
 #include "fft_kernels.h"
 
 namespace rfa {
@@ -203,63 +205,107 @@ __device__ __forceinline__ void lds_write(const float2 (&v)[16], float2 *buf, in
     }
 }
 
-template <int Q, int LOGM>
+// Workgroup-wide barrier for LDS hand-offs only: waits for this wave's LDS
+// operations (lgkmcnt) but NOT for its global loads (vmcnt), so the next
+// frame's prefetched samples stay in flight across the FFT passes.
+// (__syncthreads() would emit vmcnt(0) and drain them.)
+#ifdef RFA_SYNCTHREADS_BARRIER
+__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
+#else
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
+
+template <int Q, int LOGM, int DIAG>
 __device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid, const float2 *twc,
                                            const float2 *twf, int shift, int tw_scale) {
     using G = Geo<LOGM>;
-    butterflies<Q, LOGM>(v, tid, twc, twf, shift, tw_scale);
-    if constexpr (Q + 1 < G::NPASS) {
-        lds_write<Q, LOGM>(v, buf, tid);
-        __syncthreads();
-        lds_read<Q + 1, LOGM>(v, buf, tid);
-        __syncthreads();
-        run_passes<Q + 1, LOGM>(v, buf, tid, twc, twf, shift, tw_scale);
+    if constexpr (DIAG & 4) {  // ablation: no FFT work, one LDS round trip only
+        if constexpr (Q == 0) {
+            lds_write<0, LOGM>(v, buf, tid);
+            lds_barrier();
+            lds_read<G::NPASS - 1, LOGM>(v, buf, tid);
+            lds_barrier();
+        }
+        return;
+    } else {
+        butterflies<Q, LOGM>(v, tid, twc, twf, shift, tw_scale);
+        if constexpr (Q + 1 < G::NPASS) {
+            lds_write<Q, LOGM>(v, buf, tid);
+            lds_barrier();
+            lds_read<Q + 1, LOGM>(v, buf, tid);
+            lds_barrier();
+            run_passes<Q + 1, LOGM, DIAG>(v, buf, tid, twc, twf, shift, tw_scale);
+        }
     }
 }
 
 // ----------------------------------------------------------------- input conversion
-// One complex sample s of a frame, converted exactly as the reference LUTs do
-// (all scalings are exact powers of two, so the LUT values are reproduced bit for bit).
+// Raw sample words as loaded (converted later, so a prefetch holds 1 VGPR per
+// sample for 8/16-bit formats).
 template <int FMT>
-__device__ __forceinline__ float2 load_iq(const uint8_t *fb, int s, int n) {
-    if constexpr (FMT == 0) {  // s8: (b)/128
-        const unsigned v = *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
-        return make_float2((float)(signed char)(v & 0xff) * (1.0f / 128.0f),
-                           (float)(signed char)(v >> 8) * (1.0f / 128.0f));
-    } else if constexpr (FMT == 1) {  // u8: (b - 127.4f)/128
-        const unsigned v = *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
-        return make_float2(((float)(v & 0xff) - 127.4f) * (1.0f / 128.0f),
-                           ((float)(v >> 8) - 127.4f) * (1.0f / 128.0f));
-    } else if constexpr (FMT == 2) {  // s16le: s/32768
-        const unsigned v = *reinterpret_cast<const unsigned *>(fb + 4 * (size_t)s);
-        return make_float2((float)(short)(v & 0xffff) * (1.0f / 32768.0f),
-                           (float)(short)(v >> 16) * (1.0f / 32768.0f));
-    } else if constexpr (FMT == 3) {  // f32 interleaved
-        return *reinterpret_cast<const float2 *>(fb + 8 * (size_t)s);
-    } else {  // f32 planar: re[N] then im[N]
+struct Raw {
+    using T = float2;
+};
+template <>
+struct Raw<0> { using T = unsigned short; };
+template <>
+struct Raw<1> { using T = unsigned short; };
+template <>
+struct Raw<2> { using T = unsigned; };
+
+template <int FMT>
+__device__ __forceinline__ typename Raw<FMT>::T load_raw(const uint8_t *fb, int s, int n) {
+    if constexpr (FMT == 0 || FMT == 1) return *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
+    else if constexpr (FMT == 2) return *reinterpret_cast<const unsigned *>(fb + 4 * (size_t)s);
+    else if constexpr (FMT == 3) return *reinterpret_cast<const float2 *>(fb + 8 * (size_t)s);
+    else {
         const float *f = reinterpret_cast<const float *>(fb);
         return make_float2(f[s], f[(size_t)n + s]);
     }
 }
 
-// x * W_R^q for a wave-uniform runtime q (R in {2,4,8}).
-__device__ __forceinline__ float2 rot8(float2 x, int q8) {
-    switch (q8 & 7) {
-    case 0: return x;
-    case 1: return w16<2>(x);
-    case 2: return w16<4>(x);
-    case 3: return w16<6>(x);
-    case 4: return w16<8>(x);
-    case 5: return w16<10>(x);
-    case 6: return w16<12>(x);
-    default: return w16<14>(x);
-    }
+// Raw word -> unscaled float pair; the converter scale (1/128, 1/32768) is
+// folded into the window table by the engine.  Bit-exact with the reference
+// LUTs: s8 b/128 (Signed8BitIQConverter.java:48-50), u8 (b-127.4f)/128
+// (Unsigned8BitIQConverter.java:48-50), s16 s/32768 (Signed16BitIQConverter.kt:52-55);
+// scaling by a power of two commutes with the fp32 rounding of the window multiply.
+template <int FMT>
+__device__ __forceinline__ float2 convert_raw(typename Raw<FMT>::T v) {
+    if constexpr (FMT == 0) return make_float2((float)(signed char)(v & 0xff), (float)(signed char)(v >> 8));
+    else if constexpr (FMT == 1) return make_float2((float)(v & 0xff) - 127.4f, (float)(v >> 8) - 127.4f);
+    else if constexpr (FMT == 2) return make_float2((float)(short)(v & 0xffff), (float)(short)(v >> 16));
+    else return v;
 }
 
+template <int FMT>
+__device__ __forceinline__ typename Raw<FMT>::T synth_raw(int s) {  // ablation input
+    if constexpr (FMT == 0 || FMT == 1) return (unsigned short)(s * 2654435761u >> 16);
+    else if constexpr (FMT == 2) return (unsigned)(s * 2654435761u);
+    else return make_float2((float)(s & 255) * 0.01f, (float)((s >> 3) & 255) * 0.01f);
+}
+
+__constant__ float2 kW8[8] = {{1.f, 0.f},          {kR2, -kR2}, {0.f, -1.f}, {-kR2, -kR2},
+                               {-1.f, 0.f},         {-kR2, kR2}, {0.f, 1.f},  {kR2, kR2}};
+
 // ----------------------------------------------------------------- main kernel
-template <int LOGM, int RS, int FMT, bool COMPLEX_OUT>
-__global__ void __launch_bounds__(Geo<LOGM>::THREADS) fft_rows_kernel(FftLaunch a) {
+// Persistent: each workgroup walks work items u = blockIdx.x + k*gridDim.x.
+// RS == 1: item = SLOTS frames (one per slot); the next item's raw samples are
+//          prefetched into VGPRs while the current one is transformed.
+// RS  > 1: item = (frame, residue r); the RS items of a frame are taken by
+//          blocks that are congruent mod 8 in the same round (gridDim.x is a
+//          multiple of 8*RS), i.e. one XCD under round-robin placement.
+// Persistence (grid = CUs x occupancy, register prefetch of the next item) is
+// used where the prefetch fits the VGPR budget: RS == 1 and <= 256 threads.
+template <int LOGM, int RS>
+struct Persist {
+    static constexpr bool value = false;  // see DESIGN.md: register prefetch exceeds the VGPR budget
+};
+
+template <int LOGM, int RS, int FMT, bool COMPLEX_OUT, int DIAG>
+__global__ void __launch_bounds__(Geo<LOGM>::THREADS, 4) fft_rows_kernel(FftLaunch a) {
     using G = Geo<LOGM>;
+    constexpr bool PERSIST = Persist<LOGM, RS>::value;
+    using RT = typename Raw<FMT>::T;
     constexpr int M = G::M;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int n = M * RS;
@@ -269,143 +315,202 @@ __global__ void __launch_bounds__(Geo<LOGM>::THREADS) fft_rows_kernel(FftLaunch 
     float2 *twf = lds + nc;
     float2 *data = lds + ((nc + nf + 1) & ~1);
 
-    // copy the two-level twiddle table into LDS
     for (int e = threadIdx.x; e < nc; e += G::THREADS) twc[e] = a.tw_coarse[e];
     for (int e = threadIdx.x; e < nf; e += G::THREADS) twf[e] = a.tw_fine[e];
 
     const int slot = threadIdx.x / G::TPF;
     const int tid = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::PADM;
+    const int items = (RS == 1) ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
 
-    int frame, r;
-    if constexpr (RS == 1) {
-        frame = blockIdx.x * G::SLOTS + slot;
-        r = 0;
-    } else {
-        // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there
-        const int b = blockIdx.x;
-        const int g = b / (8 * RS), rem = b % (8 * RS);
-        r = rem / 8;
-        frame = g * 8 + (rem & 7);
+    auto decode = [&](int u, int &frame, int &r) {
+        if constexpr (RS == 1) {
+            frame = u * G::SLOTS + slot;
+            r = 0;
+        } else {
+            const int g = u / (8 * RS), rem = u - g * (8 * RS);
+            r = rem >> 3;
+            frame = g * 8 + (rem & 7);
+        }
+    };
+
+    // frame-invariant per-thread window values
+    float wv[PERSIST ? 16 : 1];
+    if constexpr (PERSIST) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) wv[t] = a.window[tid + t * G::TPF];
     }
-    const bool active = frame < a.n_frames;
-    const uint8_t *fb = a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride;
+
+    RT raw[RS == 1 ? 16 : 1];
+    auto issue = [&](int u) {
+        int fr, rr;
+        decode(u, fr, rr);
+        const bool act = fr < a.n_frames;
+        const uint8_t *fb = a.in + (size_t)(act ? fr : 0) * (size_t)a.frame_stride;
+#pragma unroll
+        for (int t = 0; t < 16; t++) {
+            const int m = tid + t * G::TPF;
+            if constexpr (DIAG & 1) raw[t] = synth_raw<FMT>(m + fr);
+            else raw[t] = load_raw<FMT>(fb, m, n);
+        }
+    };
+    if constexpr (RS == 1) {
+        if ((int)blockIdx.x < items) issue(blockIdx.x);
+    }
     __syncthreads();
 
-    // pass-0 inputs: x[tid + t*TPF], t = 0..15
-    float2 v[16];
-#pragma unroll
-    for (int t = 0; t < 16; t++) {
-        const int m = tid + t * G::TPF;
+    auto body = [&](int u) {
+        int frame, r;
+        decode(u, frame, r);
+        const bool active = frame < a.n_frames;
+        float2 v[16];
         if constexpr (RS == 1) {
-            const float w = a.window[m];
-            const float2 x = load_iq<FMT>(fb, m, n);
-            v[t] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
+#pragma unroll
+            for (int t = 0; t < 16; t++) {
+                const float2 x = convert_raw<FMT>(raw[t]);
+                const float w = PERSIST ? wv[t] : a.window[tid + t * G::TPF];
+                v[t] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
+            }
+            if constexpr (PERSIST) {
+                if (u + (int)gridDim.x < items) issue(u + gridDim.x);  // prefetch the next item
+            }
         } else {
-            float2 acc = make_float2(0.f, 0.f);
+            const uint8_t *fb = a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride;
+            float2 wr[RS];  // W_RS^{j r}: wave-uniform
 #pragma unroll
-            for (int j = 0; j < RS; j++) {
-                const int s = m + j * M;
-                const float w = a.window[s];
-                const float2 x = load_iq<FMT>(fb, s, n);
-                const float2 xw = make_float2(x.x * w, x.y * w);
-                acc = cadd(acc, rot8(xw, (j * r * (8 / RS)) & 7));
-            }
-            v[t] = (r == 0) ? acc : cmul(acc, tw(twc, twf, m * r, shift));
-        }
-    }
-
-    run_passes<0, LOGM>(v, buf, tid, twc, twf, shift, RS);
-
-    // last pass outputs: sub-bin i + t*P_last, i = tid + b*TPF
-    using PL = PassInfo<G::NPASS - 1, LOGM>;
-    if (!active) return;
-    if constexpr (COMPLEX_OUT) {
-        float2 *out = a.complex_out + (size_t)frame * n;
+            for (int j = 0; j < RS; j++) wr[j] = kW8[((j * r) * (8 / RS)) & 7];
 #pragma unroll
-        for (int b = 0; b < PL::NB; b++) {
+            for (int t = 0; t < 16; t++) {
+                const int m = tid + t * G::TPF;
+                float2 acc = make_float2(0.f, 0.f);
 #pragma unroll
-            for (int t = 0; t < PL::R; t++) {
-                const int ks = tid + b * G::TPF + t * PL::P;
-                out[r + RS * ks] = v[b * PL::R + t];
+                for (int j = 0; j < RS; j++) {
+                    const int s = m + j * M;
+                    const float w = a.window[s];
+                    RT rv;
+                    if constexpr (DIAG & 1) rv = synth_raw<FMT>(s + frame);
+                    else rv = load_raw<FMT>(fb, s, n);
+                    const float2 x = convert_raw<FMT>(rv);
+                    const float2 xw = make_float2(x.x * w, x.y * w);
+                    acc = (j == 0) ? xw : cadd(acc, cmul(xw, wr[j]));
+                }
+                v[t] = (r == 0) ? acc : cmul(acc, tw(twc, twf, m * r, shift));
+                if (t & 1) __builtin_amdgcn_sched_barrier(0);  // bound the loads in flight (VGPRs)
             }
         }
+
+        run_passes<0, LOGM, DIAG>(v, buf, tid, twc, twf, shift, RS);
+
+        using PL = PassInfo<G::NPASS - 1, LOGM>;
+        if constexpr (DIAG & 2) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) asm volatile("" ::"v"(v[q].x), "v"(v[q].y));
+            return;
+        }
+        if (!active) return;
+        if constexpr (COMPLEX_OUT) {
+            float2 *out = a.complex_out + (size_t)frame * n;
+#pragma unroll
+            for (int b = 0; b < PL::NB; b++) {
+#pragma unroll
+                for (int t = 0; t < PL::R; t++) {
+                    const int ks = tid + b * G::TPF + t * PL::P;
+                    out[r + RS * ks] = v[b * PL::R + t];
+                }
+            }
+        } else {
+            const float inv_n = 1.0f / (float)n;  // exact (power of two)
+            float *row = a.rows ? a.rows + (size_t)frame * n : nullptr;
+            float *ring = nullptr;
+            if (a.ring && frame >= a.ring_first) {
+                int rr = (a.ring_base - frame) % a.ring_rows;
+                if (rr < 0) rr += a.ring_rows;
+                ring = a.ring + (size_t)rr * n;
+            }
+            auto store = [&](float *dst, float *dst2) {
+#pragma unroll
+                for (int b = 0; b < PL::NB; b++) {
+#pragma unroll
+                    for (int t = 0; t < PL::R; t++) {
+                        const int ks = tid + b * G::TPF + t * PL::P;
+                        const int kk = r + RS * ks;
+                        const float2 x = v[b * PL::R + t];
+                        const float re = x.x * inv_n, im = x.y * inv_n;
+                        const float p = re * re + im * im;  // nativedsp.cpp:73-76
+                        const float db = 5.0f * log10f(p);   // == 10*log10(sqrt(p)), nativedsp.cpp:78
+                        const int o = (kk + (n >> 1)) & (n - 1);  // fft-shift, nativedsp.cpp:77
+                        dst[o] = db;
+                        if (dst2) dst2[o] = db;
+                    }
+                }
+            };
+            if (row && ring) store(row, ring);
+            else if (row) store(row, nullptr);
+            else if (ring) store(ring, nullptr);
+        }
+    };
+    if constexpr (PERSIST) {
+        for (int u = blockIdx.x; u < items; u += gridDim.x) body(u);
     } else {
-        const float inv_n = 1.0f / (float)n;  // exact (power of two)
-        float *row = a.rows ? a.rows + (size_t)frame * n : nullptr;
-        float *ring = nullptr;
-        if (a.ring && frame >= a.ring_first) {
-            int rr = (a.ring_base - frame) % a.ring_rows;
-            if (rr < 0) rr += a.ring_rows;
-            ring = a.ring + (size_t)rr * n;
-        }
-#pragma unroll
-        for (int b = 0; b < PL::NB; b++) {
-#pragma unroll
-            for (int t = 0; t < PL::R; t++) {
-                const int ks = tid + b * G::TPF + t * PL::P;
-                const int kk = r + RS * ks;
-                const int o = (kk + (n >> 1)) & (n - 1);
-                const float2 x = v[b * PL::R + t];
-                const float re = x.x * inv_n, im = x.y * inv_n;
-                const float p = re * re + im * im;  // nativedsp.cpp:73-76
-                const float db = 5.0f * log10f(p);   // == 10*log10(sqrt(p)), nativedsp.cpp:78
-                if (row) row[o] = db;
-                if (ring) ring[o] = db;
-            }
-        }
+        if ((int)blockIdx.x < items) body(blockIdx.x);
     }
 }
 
 // ----------------------------------------------------------------- dispatch
-template <int LOGM, int RS, int FMT, bool CO>
+static int g_cus = 0;
+
+template <int LOGM, int RS, int FMT, bool CO, int DIAG>
 static hipError_t launch_one(const FftLaunch &a) {
     using G = Geo<LOGM>;
+    auto kern = &fft_rows_kernel<LOGM, RS, FMT, CO, DIAG>;
     const int n = G::M * RS;
     const int nc = n >> a.tw_shift, nf = 1 << a.tw_shift;
     const size_t lds = (size_t)(((nc + nf + 1) & ~1) + G::SLOTS * G::PADM) * sizeof(float2);
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&fft_rows_kernel<LOGM, RS, FMT, CO>),
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
-        attr_set = true;
+        if (g_cus == 0) {
+            int dev = 0;
+            hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) g_cus = 256;
+        }
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, G::THREADS, lds) != hipSuccess || occ < 1) occ = 1;
+        per_cu = occ;
     }
-    unsigned blocks;
-    if (RS == 1) blocks = (unsigned)((a.n_frames + G::SLOTS - 1) / G::SLOTS);
-    else blocks = (unsigned)(((a.n_frames + 7) / 8) * 8 * RS);
-    if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((fft_rows_kernel<LOGM, RS, FMT, CO>), dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
+    const int items = (RS == 1) ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    if (items <= 0) return hipSuccess;
+    int grid = items;
+    if (Persist<LOGM, RS>::value) grid = std::min(items, g_cus * per_cu);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), lds, a.stream, a);
     return hipGetLastError();
 }
 
 template <int LOGM, int RS, bool CO>
 static hipError_t by_fmt(const FftLaunch &a) {
-    switch (a.fmt) {
-    case 0: return launch_one<LOGM, RS, 0, CO>(a);
-    case 1: return launch_one<LOGM, RS, 1, CO>(a);
-    case 2: return launch_one<LOGM, RS, 2, CO>(a);
-    case 3: return launch_one<LOGM, RS, 3, CO>(a);
-    case 4: return launch_one<LOGM, RS, 4, CO>(a);
-    default: return hipErrorInvalidValue;
+    if constexpr (!CO) {
+        if (a.diag) {  // ablation builds (profiling only): 16K/64K, s8 and f32
+            if constexpr (LOGM == 14 && (RS == 1 || RS == 4)) {
+#define RFA_DIAG(D)                                                   \
+    case D:                                                           \
+        return a.fmt == 0 ? launch_one<LOGM, RS, 0, false, D>(a)     \
+                          : launch_one<LOGM, RS, 3, false, D>(a);
+                if (a.fmt != 0 && a.fmt != 3) return hipErrorInvalidValue;
+                switch (a.diag) { RFA_DIAG(1) RFA_DIAG(2) RFA_DIAG(3) RFA_DIAG(4) RFA_DIAG(6) RFA_DIAG(7)
+                default: return hipErrorInvalidValue; }
+#undef RFA_DIAG
+            }
+            return hipErrorInvalidValue;
+        }
     }
-}
-
-template <bool CO>
-static hipError_t by_size(const FftLaunch &a) {
-    switch (a.logn) {
-    case 6: return by_fmt<6, 1, CO>(a);
-    case 7: return by_fmt<7, 1, CO>(a);
-    case 8: return by_fmt<8, 1, CO>(a);
-    case 9: return by_fmt<9, 1, CO>(a);
-    case 10: return by_fmt<10, 1, CO>(a);
-    case 11: return by_fmt<11, 1, CO>(a);
-    case 12: return by_fmt<12, 1, CO>(a);
-    case 13: return by_fmt<13, 1, CO>(a);
-    case 14: return by_fmt<14, 1, CO>(a);
-    case 15: return by_fmt<14, 2, CO>(a);
-    case 16: return by_fmt<14, 4, CO>(a);
-    case 17: return by_fmt<14, 8, CO>(a);
+    switch (a.fmt) {
+    case 0: return launch_one<LOGM, RS, 0, CO, 0>(a);
+    case 1: return launch_one<LOGM, RS, 1, CO, 0>(a);
+    case 2: return launch_one<LOGM, RS, 2, CO, 0>(a);
+    case 3: return launch_one<LOGM, RS, 3, CO, 0>(a);
+    case 4: return launch_one<LOGM, RS, 4, CO, 0>(a);
     default: return hipErrorInvalidValue;
     }
 }
@@ -415,14 +520,36 @@ hipError_t launch_fft(const FftLaunch &a) {
         if (a.fmt != 3) return hipErrorInvalidValue;
         switch (a.logn) {  // complex output: f32 interleaved only
 #define RFA_CO(L, RS) \
-    case (L + (RS == 1 ? 0 : (RS == 2 ? 1 : (RS == 4 ? 2 : 3)))): return launch_one<L, RS, 3, true>(a);
+    case (L + (RS == 1 ? 0 : (RS == 2 ? 1 : (RS == 4 ? 2 : 3)))): return launch_one<L, RS, 3, true, 0>(a);
             RFA_CO(6, 1) RFA_CO(7, 1) RFA_CO(8, 1) RFA_CO(9, 1) RFA_CO(10, 1) RFA_CO(11, 1) RFA_CO(12, 1)
             RFA_CO(13, 1) RFA_CO(14, 1) RFA_CO(14, 2) RFA_CO(14, 4) RFA_CO(14, 8)
 #undef RFA_CO
         default: return hipErrorInvalidValue;
         }
     }
-    return by_size<false>(a);
+    if (a.max_logm == 13) {  // experiment: 8K sub-FFTs (2 workgroups per CU) with a wider split
+        switch (a.logn) {
+        case 14: return by_fmt<13, 2, false>(a);
+        case 15: return by_fmt<13, 4, false>(a);
+        case 16: return by_fmt<13, 8, false>(a);
+        default: break;
+        }
+    }
+    switch (a.logn) {
+    case 6: return by_fmt<6, 1, false>(a);
+    case 7: return by_fmt<7, 1, false>(a);
+    case 8: return by_fmt<8, 1, false>(a);
+    case 9: return by_fmt<9, 1, false>(a);
+    case 10: return by_fmt<10, 1, false>(a);
+    case 11: return by_fmt<11, 1, false>(a);
+    case 12: return by_fmt<12, 1, false>(a);
+    case 13: return by_fmt<13, 1, false>(a);
+    case 14: return by_fmt<14, 1, false>(a);
+    case 15: return by_fmt<14, 2, false>(a);
+    case 16: return by_fmt<14, 4, false>(a);
+    case 17: return by_fmt<14, 8, false>(a);
+    default: return hipErrorInvalidValue;
+    }
 }
 
 // ----------------------------------------------------------------- state / ring kernels
@@ -435,7 +562,14 @@ __global__ void state_kernel(StateLaunch a) {
     float em = a.ema ? a.ema[bin] : 0.f;
     const float al = a.ema_alpha;
     for (int f = 0; f < a.n_frames; f++) {
-        const float x = a.rows[(size_t)f * a.row_stride + bin];
+        size_t row;
+        if (a.ring_rows > 0) {
+            int rr = (a.ring_base - f) % a.ring_rows;
+            row = (size_t)(rr < 0 ? rr + a.ring_rows : rr) * a.n;
+        } else {
+            row = (size_t)((long long)f * a.row_stride);
+        }
+        const float x = a.rows[row + bin];
         pk = fmaxf(pk, x);
         em = (em > -INFINITY) ? em + al * (x - em) : x;
     }

@@ -108,7 +108,11 @@ class SpectrumEngine:
         self.process_device(t.data_ptr(), n_frames, frame_stride, rows.data_ptr() if rows is not None else None)
 
     def set_stream(self, stream_ptr: int | None) -> None:
-        self._check(_lib.lib().rfa_set_stream(self._h, stream_ptr), "rfa_set_stream")
+        """Enqueue on exactly this hipStream_t (0/None = HIP null stream)."""
+        self._check(_lib.lib().rfa_set_stream(self._h, stream_ptr or None), "rfa_set_stream")
+
+    def use_own_stream(self) -> None:
+        self._check(_lib.lib().rfa_use_own_stream(self._h), "rfa_use_own_stream")
 
     def synchronize(self) -> None:
         self._check(_lib.lib().rfa_synchronize(self._h), "rfa_synchronize")

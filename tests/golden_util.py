@@ -57,6 +57,16 @@ def expected(spec: dict):
     return np.load(path, allow_pickle=False)
 
 
+def assert_same_peak_bins(got: np.ndarray, exp_argmax) -> None:
+    """Bit-exact bin ordering: the reference's peak bin is our peak bin.  An
+    exact tie (e.g. a tone at k+0.5 under a symmetric window) is decided by
+    rounding on either side, so the reference's bin only has to be within
+    DB_TOL of our maximum."""
+    got = np.atleast_2d(got)
+    for row, a in zip(got, exp_argmax):
+        assert row[a] >= row.max() - DB_TOL, (int(np.argmax(row)), a)
+
+
 def db_diff(got: np.ndarray, exp: np.ndarray) -> float:
     """Max |dB difference| over bins within FLOOR_DB of the row's total level.
 
