@@ -30,6 +30,9 @@ struct rfa_handle {
     float *d_window = nullptr;
     float *d_window_none = nullptr;   // all ones (already-windowed f32 seams)
     float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
+    float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
+    float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17)
+    int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     float2 *d_twc = nullptr, *d_twf = nullptr;
@@ -183,6 +186,10 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_fine = h->d_twf;
     a.tw_shift = h->tw_shift;
     a.diag = h->diag;
+    a.wide_tw = h->d_wide_tw;
+    a.variant = h->variant;
+    if (a.window == h->d_window) a.window_il = h->d_window_il;
+    else if (h->logn > 14) a.variant = 1;  // seam windows have no interleaved copy: narrow kernel
     a.max_logm = h->max_logm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->profile) {
@@ -297,6 +304,40 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMalloc(tabs[i], n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(*tabs[i], src[i], n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
     }
+    if (n > 16384) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
+        const int m_sub = 16384, rs = n / m_sub;
+        std::vector<float> il(n);
+        for (int m = 0; m < m_sub; m++)
+            for (int j = 0; j < rs; j++) il[(size_t)m * rs + j] = w[(size_t)m + (size_t)j * m_sub];
+        if (hipMalloc(&h->d_window_il, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(RFA_ERR_HIP);
+    }
+    if (rfa::wide_supported(logn)) {
+        const int lm = logn == 13 ? 13 : 14, m = 1 << lm, rs = n / m, r1 = lm == 14 ? 32 : 16;
+        auto w = [](double num, double den) {  // exp(-2 pi i num/den), correctly rounded
+            const double a = -2.0 * M_PI * num / den;
+            return make_float2((float)std::cos(a), (float)std::sin(a));
+        };
+        std::vector<float2> blob;
+        // rows padded by one entry (bank-conflict-free LDS reads, fft_wide.hip WGeo)
+        for (int k = 0; k < 32; k++)
+            for (int t = 0; t <= r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
+        for (int th = 0; th < 16; th++)
+            for (int t = 0; t <= 16; t++) blob.push_back(w(16.0 * t * th, m));
+        for (int tl = 0; tl < 16; tl++)
+            for (int t = 0; t <= 16; t++) blob.push_back(w((double)t * tl, m));
+        if (rs > 1) {
+            for (int r = 0; r < rs; r++)
+                for (int mp = 0; mp < 512; mp++) blob.push_back(w((double)mp * r, n));
+            for (int r = 0; r < rs; r++)
+                for (int t = 0; t < 32; t++) blob.push_back(w(512.0 * t * r, n));
+        }
+        if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMemcpy(h->d_wide_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(RFA_ERR_HIP);
+    }
+    if (const char *d = std::getenv("RFA_KERNEL")) h->variant = std::string(d) == "narrow" ? 1 : 0;
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
     if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
@@ -340,6 +381,8 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_window);
     hipFree(h->d_window_none);
     hipFree(h->d_window_black);
+    hipFree(h->d_window_il);
+    hipFree(h->d_wide_tw);
     hipFree(h->d_twc);
     hipFree(h->d_twf);
     hipFree(h->d_ring);

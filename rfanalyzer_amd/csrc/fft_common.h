@@ -1,0 +1,300 @@
+// Shared device helpers of the gfx950 spectrum kernels: complex arithmetic,
+// in-register DFTs, twiddle lookup, raw IQ conversion, LDS-only barrier.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <utility>
+
+// Pure-math helpers are host+device so tests/csrc can check them on the CPU.
+#define RFA_HD __host__ __device__ __forceinline__
+
+namespace rfa {
+
+
+// ----------------------------------------------------------------- complex helpers
+RFA_HD float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+RFA_HD float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+RFA_HD float2 cmul(float2 a, float2 b) {
+    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+RFA_HD float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
+RFA_HD float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }  // * (+i)
+
+// exp(-2*pi*i*m/16), correctly rounded fp32 constants.
+constexpr float kC1 = 0.923879532511286756f;  // cos(pi/8)
+constexpr float kS1 = 0.382683432365089772f;  // sin(pi/8)
+constexpr float kR2 = 0.707106781186547524f;  // sqrt(1/2)
+
+// x * W_16^m (m in 0..15), constant-folded per call site.
+template <int m>
+RFA_HD float2 w16(float2 x) {
+    constexpr int q = m & 15;
+    if constexpr (q == 0) return x;
+    else if constexpr (q == 4) return mul_mi(x);
+    else if constexpr (q == 8) return make_float2(-x.x, -x.y);
+    else if constexpr (q == 12) return mul_pi(x);
+    else if constexpr (q == 2) return make_float2((x.x + x.y) * kR2, (x.y - x.x) * kR2);
+    else if constexpr (q == 6) return make_float2((x.y - x.x) * kR2, -(x.x + x.y) * kR2);
+    else if constexpr (q == 10) return make_float2(-(x.x + x.y) * kR2, (x.x - x.y) * kR2);
+    else if constexpr (q == 14) return make_float2((x.x - x.y) * kR2, (x.x + x.y) * kR2);
+    else {
+        constexpr float c[16] = {1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1, 0, kS1, kR2, kC1};
+        constexpr float s[16] = {0, kS1, kR2, kC1, 1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1};
+        // W = cos - i sin
+        return cmul(x, make_float2(c[q], -s[q]));
+    }
+}
+
+// In-register forward DFTs, natural order in and out.
+RFA_HD void dft2(float2 &a, float2 &b) {
+    float2 t = a;
+    a = cadd(t, b);
+    b = csub(t, b);
+}
+RFA_HD void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
+    float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
+    x0 = cadd(s02, s13);
+    x2 = csub(s02, s13);
+    x1 = cadd(d02, mul_mi(d13));
+    x3 = cadd(d02, mul_pi(d13));
+}
+
+template <int R>
+RFA_HD void dft(float2 *u);
+
+template <>
+RFA_HD void dft<2>(float2 *u) { dft2(u[0], u[1]); }
+template <>
+RFA_HD void dft<4>(float2 *u) { dft4(u[0], u[1], u[2], u[3]); }
+template <>
+RFA_HD void dft<8>(float2 *u) {
+    // t = 2*t1 + t2; DFT-4 over t1, twiddle W_8^{t2 q1} (= W_16^{2 t2 q1}), DFT-2 over t2.
+    dft4(u[0], u[2], u[4], u[6]);
+    dft4(u[1], u[3], u[5], u[7]);
+    u[3] = w16<2>(u[3]);
+    u[5] = w16<4>(u[5]);
+    u[7] = w16<6>(u[7]);
+    dft2(u[0], u[1]);
+    dft2(u[2], u[3]);
+    dft2(u[4], u[5]);
+    dft2(u[6], u[7]);
+    // position 2*q1 + q2 holds Y[q1 + 4 q2]
+    float2 y[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) y[q] = u[2 * (q & 3) + (q >> 2)];
+#pragma unroll
+    for (int q = 0; q < 8; q++) u[q] = y[q];
+}
+template <>
+RFA_HD void dft<16>(float2 *u) {
+    // t = 4*t1 + t2; DFT-4 over t1, twiddle W_16^{t2 q1}, DFT-4 over t2.
+    dft4(u[0], u[4], u[8], u[12]);
+    dft4(u[1], u[5], u[9], u[13]);
+    dft4(u[2], u[6], u[10], u[14]);
+    dft4(u[3], u[7], u[11], u[15]);
+    u[5] = w16<1>(u[5]);
+    u[6] = w16<2>(u[6]);
+    u[7] = w16<3>(u[7]);
+    u[9] = w16<2>(u[9]);
+    u[10] = w16<4>(u[10]);
+    u[11] = w16<6>(u[11]);
+    u[13] = w16<3>(u[13]);
+    u[14] = w16<6>(u[14]);
+    u[15] = w16<9>(u[15]);
+    dft4(u[0], u[1], u[2], u[3]);
+    dft4(u[4], u[5], u[6], u[7]);
+    dft4(u[8], u[9], u[10], u[11]);
+    dft4(u[12], u[13], u[14], u[15]);
+    // position 4*q1 + q2 holds Y[q1 + 4 q2]
+    float2 y[16];
+#pragma unroll
+    for (int q = 0; q < 16; q++) y[q] = u[4 * (q & 3) + (q >> 2)];
+#pragma unroll
+    for (int q = 0; q < 16; q++) u[q] = y[q];
+}
+
+// cos/sin(2*pi*m/64), correctly rounded fp32 (generated)
+constexpr float kCos64[64] = {1.0f, 0.99518472f, 0.980785251f, 0.956940353f, 0.923879504f, 0.881921291f, 0.831469595f, 0.773010433f, 0.707106769f, 0.634393275f, 0.555570245f, 0.471396744f, 0.382683426f, 0.290284663f, 0.195090324f, 0.0980171412f, 0.0f, -0.0980171412f, -0.195090324f, -0.290284663f, -0.382683426f, -0.471396744f, -0.555570245f, -0.634393275f, -0.707106769f, -0.773010433f, -0.831469595f, -0.881921291f, -0.923879504f, -0.956940353f, -0.980785251f, -0.99518472f, -1.0f, -0.99518472f, -0.980785251f, -0.956940353f, -0.923879504f, -0.881921291f, -0.831469595f, -0.773010433f, -0.707106769f, -0.634393275f, -0.555570245f, -0.471396744f, -0.382683426f, -0.290284663f, -0.195090324f, -0.0980171412f, 0.0f, 0.0980171412f, 0.195090324f, 0.290284663f, 0.382683426f, 0.471396744f, 0.555570245f, 0.634393275f, 0.707106769f, 0.773010433f, 0.831469595f, 0.881921291f, 0.923879504f, 0.956940353f, 0.980785251f, 0.99518472f};
+constexpr float kSin64[64] = {0.0f, 0.0980171412f, 0.195090324f, 0.290284663f, 0.382683426f, 0.471396744f, 0.555570245f, 0.634393275f, 0.707106769f, 0.773010433f, 0.831469595f, 0.881921291f, 0.923879504f, 0.956940353f, 0.980785251f, 0.99518472f, 1.0f, 0.99518472f, 0.980785251f, 0.956940353f, 0.923879504f, 0.881921291f, 0.831469595f, 0.773010433f, 0.707106769f, 0.634393275f, 0.555570245f, 0.471396744f, 0.382683426f, 0.290284663f, 0.195090324f, 0.0980171412f, 0.0f, -0.0980171412f, -0.195090324f, -0.290284663f, -0.382683426f, -0.471396744f, -0.555570245f, -0.634393275f, -0.707106769f, -0.773010433f, -0.831469595f, -0.881921291f, -0.923879504f, -0.956940353f, -0.980785251f, -0.99518472f, -1.0f, -0.99518472f, -0.980785251f, -0.956940353f, -0.923879504f, -0.881921291f, -0.831469595f, -0.773010433f, -0.707106769f, -0.634393275f, -0.555570245f, -0.471396744f, -0.382683426f, -0.290284663f, -0.195090324f, -0.0980171412f};
+
+// x * W_64^m (m constant), W = exp(-2*pi*i/64); multiples of 4 use the W_16 forms.
+template <int m>
+RFA_HD float2 w64(float2 x) {
+    constexpr int q = m & 63;
+    if constexpr ((q & 3) == 0) return w16<q / 4>(x);
+    else return cmul(x, make_float2(kCos64[q], -kSin64[q]));
+}
+
+template <>
+RFA_HD void dft<32>(float2 *u) {
+    // t = 16*t1 + t2 (t1 < 2): DFT-2 over t1, twiddle W_32^{t2 q1} = W_64^{2 t2 q1}, DFT-16 over t2.
+#pragma unroll
+    for (int t2 = 0; t2 < 16; t2++) dft2(u[t2], u[16 + t2]);
+    u[17] = w64<2>(u[17]); u[18] = w64<4>(u[18]); u[19] = w64<6>(u[19]); u[20] = w64<8>(u[20]);
+    u[21] = w64<10>(u[21]); u[22] = w64<12>(u[22]); u[23] = w64<14>(u[23]); u[24] = w64<16>(u[24]);
+    u[25] = w64<18>(u[25]); u[26] = w64<20>(u[26]); u[27] = w64<22>(u[27]); u[28] = w64<24>(u[28]);
+    u[29] = w64<26>(u[29]); u[30] = w64<28>(u[30]); u[31] = w64<30>(u[31]);
+    dft<16>(u);
+    dft<16>(u + 16);
+    // position 16*q1 + q2 holds Y[q1 + 2 q2]
+    float2 y[32];
+#pragma unroll
+    for (int q = 0; q < 32; q++) y[q] = u[16 * (q & 1) + (q >> 1)];
+#pragma unroll
+    for (int q = 0; q < 32; q++) u[q] = y[q];
+}
+
+template <int T2, int Q1>
+RFA_HD void tw64_step(float2 *u) {
+    u[16 * Q1 + T2] = w64<T2 * Q1>(u[16 * Q1 + T2]);
+}
+template <int T2>
+RFA_HD void tw64_col(float2 *u) {
+    tw64_step<T2, 1>(u);
+    tw64_step<T2, 2>(u);
+    tw64_step<T2, 3>(u);
+}
+template <int... T2s>
+RFA_HD void tw64_all(float2 *u, std::integer_sequence<int, T2s...>) {
+    (tw64_col<T2s>(u), ...);
+}
+
+template <>
+RFA_HD void dft<64>(float2 *u) {
+    // t = 16*t1 + t2 (t1 < 4): DFT-4 over t1, twiddle W_64^{t2 q1}, DFT-16 over t2.
+#pragma unroll
+    for (int t2 = 0; t2 < 16; t2++) dft4(u[t2], u[16 + t2], u[32 + t2], u[48 + t2]);
+    tw64_all(u, std::make_integer_sequence<int, 16>{});
+    dft<16>(u);
+    dft<16>(u + 16);
+    dft<16>(u + 32);
+    dft<16>(u + 48);
+    // position 16*q1 + q2 holds Y[q1 + 4 q2]
+    float2 y[64];
+#pragma unroll
+    for (int q = 0; q < 64; q++) y[q] = u[16 * (q & 3) + (q >> 2)];
+#pragma unroll
+    for (int q = 0; q < 64; q++) u[q] = y[q];
+}
+
+// Twiddle W_N^s from the two-level LDS table.
+__device__ __forceinline__ float2 tw(const float2 *twc, const float2 *twf, int s, int shift) {
+    return cmul(twc[s >> shift], twf[s & ((1 << shift) - 1)]);
+}
+
+// Workgroup-wide barrier for LDS hand-offs only: waits for this wave's LDS
+// operations (lgkmcnt) but NOT for its global loads (vmcnt), so the next
+// frame's prefetched samples stay in flight across the FFT passes.
+// (__syncthreads() would emit vmcnt(0) and drain them.)
+#ifdef RFA_SYNCTHREADS_BARRIER
+__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
+#else
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+#endif
+
+// ----------------------------------------------------------------- input conversion
+// Raw sample words as loaded (converted later, so a prefetch holds 1 VGPR per
+// sample for 8/16-bit formats).
+template <int FMT>
+struct Raw {
+    using T = float2;
+};
+template <>
+struct Raw<0> { using T = unsigned short; };
+template <>
+struct Raw<1> { using T = unsigned short; };
+template <>
+struct Raw<2> { using T = unsigned; };
+
+template <int FMT>
+__device__ __forceinline__ typename Raw<FMT>::T load_raw(const uint8_t *fb, int s, int n) {
+    if constexpr (FMT == 0 || FMT == 1) return *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
+    else if constexpr (FMT == 2) return *reinterpret_cast<const unsigned *>(fb + 4 * (size_t)s);
+    else if constexpr (FMT == 3) return *reinterpret_cast<const float2 *>(fb + 8 * (size_t)s);
+    else {
+        const float *f = reinterpret_cast<const float *>(fb);
+        return make_float2(f[s], f[(size_t)n + s]);
+    }
+}
+
+// Raw word -> unscaled float pair; the converter scale (1/128, 1/32768) is
+// folded into the window table by the engine.  Bit-exact with the reference
+// LUTs: s8 b/128 (Signed8BitIQConverter.java:48-50), u8 (b-127.4f)/128
+// (Unsigned8BitIQConverter.java:48-50), s16 s/32768 (Signed16BitIQConverter.kt:52-55);
+// scaling by a power of two commutes with the fp32 rounding of the window multiply.
+template <int FMT>
+__device__ __forceinline__ float2 convert_raw(typename Raw<FMT>::T v) {
+    if constexpr (FMT == 0) return make_float2((float)(signed char)(v & 0xff), (float)(signed char)(v >> 8));
+    else if constexpr (FMT == 1) return make_float2((float)(v & 0xff) - 127.4f, (float)(v >> 8) - 127.4f);
+    else if constexpr (FMT == 2) return make_float2((float)(short)(v & 0xffff), (float)(short)(v >> 16));
+    else return v;
+}
+
+template <int FMT>
+__device__ __forceinline__ typename Raw<FMT>::T synth_raw(int s) {  // ablation input
+    if constexpr (FMT == 0 || FMT == 1) return (unsigned short)(s * 2654435761u >> 16);
+    else if constexpr (FMT == 2) return (unsigned)(s * 2654435761u);
+    else return make_float2((float)(s & 255) * 0.01f, (float)((s >> 3) & 255) * 0.01f);
+}
+
+static __constant__ float2 kW8[8] = {{1.f, 0.f},          {kR2, -kR2}, {0.f, -1.f}, {-kR2, -kR2},
+                               {-1.f, 0.f},         {-kR2, kR2}, {0.f, 1.f},  {kR2, kR2}};
+
+
+// ----------------------------------------------------------------- buffer access
+// Raw buffer loads/stores: one 32-bit VGPR offset per lane plus a wave-uniform
+// SGPR offset, so the 64+ memory operations of a thread need no 64-bit address
+// registers.  Out-of-range accesses (num_records) read 0 / are dropped.
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const void *p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__device__ __forceinline__ float2 buf_load_f32x2(rsrc_t rs, int voff, int soff);
+
+// One raw sample at byte offset voff + soff of the frame (formats as Raw<FMT>).
+template <int FMT>
+__device__ __forceinline__ typename Raw<FMT>::T buf_load_raw(rsrc_t rs, int voff, int soff, int planar_im_off) {
+    if constexpr (FMT == 0 || FMT == 1) return (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0);
+    else if constexpr (FMT == 2) return (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
+    else if constexpr (FMT == 3) {
+        return buf_load_f32x2(rs, voff, soff);
+    } else {
+        const float re = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+        const float im = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff + planar_im_off, 0));
+        return make_float2(re, im);
+    }
+}
+__device__ __forceinline__ float buf_load_f32(rsrc_t rs, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));
+}
+// NOTE: index the b64 result only after bit-casting it to a float vector --
+// element access on the builtin's own return type loads a single dword
+// (hipcc, ROCm 7.2).
+typedef float rfa_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2 buf_load_f32x2(rsrc_t rs, int voff, int soff) {
+    const rfa_f32x2 v = __builtin_bit_cast(rfa_f32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0));
+    return make_float2(v.x, v.y);
+}
+__device__ __forceinline__ void buf_store_f32(float x, rsrc_t rs, int voff, int soff) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), rs, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, int soff) {
+    typedef int i32x2 __attribute__((ext_vector_type(2)));
+    i32x2 v = {__builtin_bit_cast(int, x.x), __builtin_bit_cast(int, x.y)};
+    __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, soff, 0);
+}
+
+// 10*log10(sqrt(p)) (nativedsp.cpp:78) = (5*log10(2)) * log2(p) on the hardware
+// log2 (v_log_f32).  It flushes denormal inputs, so those are pre-scaled by
+// 2^24; log2(0) = -inf as in the reference.
+__device__ __forceinline__ float db_from_power(float p) {
+    const bool den = p < 1.17549435e-38f;
+    const float l = __builtin_amdgcn_logf(den ? p * 16777216.0f : p) - (den ? 24.0f : 0.0f);
+    return l * 1.50514997831990598f;
+}
+
+}  // namespace rfa

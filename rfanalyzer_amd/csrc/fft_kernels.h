@@ -21,6 +21,10 @@ struct FftLaunch {
     int fmt = 0;   // rfa_input_format
     int logn = 0;  // N = 1 << logn
     const float *window = nullptr;  // N floats (device); all ones for RFA_WINDOW_NONE
+    const float *window_il = nullptr;
+    // wide kernel twiddle blob (exact, from double): pass-1 [32][R1] | pass-2 A,B [16][16] |
+    // pre-stage pre_a [RS][512] | pre_b [RS][32]   (DESIGN.md "Twiddles")
+    const float2 *wide_tw = nullptr;  // N > 16384: window[m + j*M] at [m*RS + j] (wide kernel pre-stage)
     // twiddle table W_N^s = coarse[s >> tw_shift] * fine[s & ((1<<tw_shift)-1)]
     const float2 *tw_coarse = nullptr;
     const float2 *tw_fine = nullptr;
@@ -32,6 +36,7 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
     int max_logm = 14;  // largest sub-FFT per workgroup (13 = experiment: 2 workgroups per CU)
     int diag = 0;  // ablation variant (profiling only): 1 no loads, 2 no stores, 4 no FFT passes
     hipStream_t stream = nullptr;
@@ -39,6 +44,9 @@ struct FftLaunch {
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
 hipError_t launch_fft(const FftLaunch &a);
+// The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
+bool wide_supported(int logn);
+hipError_t launch_fft_wide(const FftLaunch &a);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at
 // rows + f*row_stride, or, when ring_rows > 0, at rows + ((ring_base - f) mod ring_rows)*n

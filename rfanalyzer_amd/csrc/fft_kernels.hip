@@ -20,112 +20,10 @@
 
 #include <algorithm>
 
+#include "fft_common.h"
 #include "fft_kernels.h"
 
 namespace rfa {
-
-// ----------------------------------------------------------------- complex helpers
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
-}
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
-__device__ __forceinline__ float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }  // * (+i)
-
-// exp(-2*pi*i*m/16), correctly rounded fp32 constants.
-constexpr float kC1 = 0.923879532511286756f;  // cos(pi/8)
-constexpr float kS1 = 0.382683432365089772f;  // sin(pi/8)
-constexpr float kR2 = 0.707106781186547524f;  // sqrt(1/2)
-
-// x * W_16^m (m in 0..15), constant-folded per call site.
-template <int m>
-__device__ __forceinline__ float2 w16(float2 x) {
-    constexpr int q = m & 15;
-    if constexpr (q == 0) return x;
-    else if constexpr (q == 4) return mul_mi(x);
-    else if constexpr (q == 8) return make_float2(-x.x, -x.y);
-    else if constexpr (q == 12) return mul_pi(x);
-    else if constexpr (q == 2) return make_float2((x.x + x.y) * kR2, (x.y - x.x) * kR2);
-    else if constexpr (q == 6) return make_float2((x.y - x.x) * kR2, -(x.x + x.y) * kR2);
-    else if constexpr (q == 10) return make_float2(-(x.x + x.y) * kR2, (x.x - x.y) * kR2);
-    else if constexpr (q == 14) return make_float2((x.x - x.y) * kR2, (x.x + x.y) * kR2);
-    else {
-        constexpr float c[16] = {1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1, 0, kS1, kR2, kC1};
-        constexpr float s[16] = {0, kS1, kR2, kC1, 1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1};
-        // W = cos - i sin
-        return cmul(x, make_float2(c[q], -s[q]));
-    }
-}
-
-// In-register forward DFTs, natural order in and out.
-__device__ __forceinline__ void dft2(float2 &a, float2 &b) {
-    float2 t = a;
-    a = cadd(t, b);
-    b = csub(t, b);
-}
-__device__ __forceinline__ void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
-    float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
-    x0 = cadd(s02, s13);
-    x2 = csub(s02, s13);
-    x1 = cadd(d02, mul_mi(d13));
-    x3 = cadd(d02, mul_pi(d13));
-}
-
-template <int R>
-__device__ __forceinline__ void dft(float2 *u);
-
-template <>
-__device__ __forceinline__ void dft<2>(float2 *u) { dft2(u[0], u[1]); }
-template <>
-__device__ __forceinline__ void dft<4>(float2 *u) { dft4(u[0], u[1], u[2], u[3]); }
-template <>
-__device__ __forceinline__ void dft<8>(float2 *u) {
-    // t = 2*t1 + t2; DFT-4 over t1, twiddle W_8^{t2 q1} (= W_16^{2 t2 q1}), DFT-2 over t2.
-    dft4(u[0], u[2], u[4], u[6]);
-    dft4(u[1], u[3], u[5], u[7]);
-    u[3] = w16<2>(u[3]);
-    u[5] = w16<4>(u[5]);
-    u[7] = w16<6>(u[7]);
-    dft2(u[0], u[1]);
-    dft2(u[2], u[3]);
-    dft2(u[4], u[5]);
-    dft2(u[6], u[7]);
-    // position 2*q1 + q2 holds Y[q1 + 4 q2]
-    float2 y[8];
-#pragma unroll
-    for (int q = 0; q < 8; q++) y[q] = u[2 * (q & 3) + (q >> 2)];
-#pragma unroll
-    for (int q = 0; q < 8; q++) u[q] = y[q];
-}
-template <>
-__device__ __forceinline__ void dft<16>(float2 *u) {
-    // t = 4*t1 + t2; DFT-4 over t1, twiddle W_16^{t2 q1}, DFT-4 over t2.
-    dft4(u[0], u[4], u[8], u[12]);
-    dft4(u[1], u[5], u[9], u[13]);
-    dft4(u[2], u[6], u[10], u[14]);
-    dft4(u[3], u[7], u[11], u[15]);
-    u[5] = w16<1>(u[5]);
-    u[6] = w16<2>(u[6]);
-    u[7] = w16<3>(u[7]);
-    u[9] = w16<2>(u[9]);
-    u[10] = w16<4>(u[10]);
-    u[11] = w16<6>(u[11]);
-    u[13] = w16<3>(u[13]);
-    u[14] = w16<6>(u[14]);
-    u[15] = w16<9>(u[15]);
-    dft4(u[0], u[1], u[2], u[3]);
-    dft4(u[4], u[5], u[6], u[7]);
-    dft4(u[8], u[9], u[10], u[11]);
-    dft4(u[12], u[13], u[14], u[15]);
-    // position 4*q1 + q2 holds Y[q1 + 4 q2]
-    float2 y[16];
-#pragma unroll
-    for (int q = 0; q < 16; q++) y[q] = u[4 * (q & 3) + (q >> 2)];
-#pragma unroll
-    for (int q = 0; q < 16; q++) u[q] = y[q];
-}
-
 // ----------------------------------------------------------------- geometry
 template <int LOGM>
 struct Geo {
@@ -151,11 +49,6 @@ struct PassInfo {
     static constexpr int P = 1 << PREV_LOG;  // product of earlier radices
     static constexpr int NB = 16 / R;        // butterflies per thread
 };
-
-// Twiddle W_N^s from the two-level LDS table.
-__device__ __forceinline__ float2 tw(const float2 *twc, const float2 *twf, int s, int shift) {
-    return cmul(twc[s >> shift], twf[s & ((1 << shift) - 1)]);
-}
 
 // Read the inputs of pass Q from LDS into v.
 template <int Q, int LOGM>
@@ -205,16 +98,6 @@ __device__ __forceinline__ void lds_write(const float2 (&v)[16], float2 *buf, in
     }
 }
 
-// Workgroup-wide barrier for LDS hand-offs only: waits for this wave's LDS
-// operations (lgkmcnt) but NOT for its global loads (vmcnt), so the next
-// frame's prefetched samples stay in flight across the FFT passes.
-// (__syncthreads() would emit vmcnt(0) and drain them.)
-#ifdef RFA_SYNCTHREADS_BARRIER
-__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
-#else
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
-
 template <int Q, int LOGM, int DIAG>
 __device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid, const float2 *twc,
                                            const float2 *twf, int shift, int tw_scale) {
@@ -238,54 +121,6 @@ __device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid
         }
     }
 }
-
-// ----------------------------------------------------------------- input conversion
-// Raw sample words as loaded (converted later, so a prefetch holds 1 VGPR per
-// sample for 8/16-bit formats).
-template <int FMT>
-struct Raw {
-    using T = float2;
-};
-template <>
-struct Raw<0> { using T = unsigned short; };
-template <>
-struct Raw<1> { using T = unsigned short; };
-template <>
-struct Raw<2> { using T = unsigned; };
-
-template <int FMT>
-__device__ __forceinline__ typename Raw<FMT>::T load_raw(const uint8_t *fb, int s, int n) {
-    if constexpr (FMT == 0 || FMT == 1) return *reinterpret_cast<const unsigned short *>(fb + 2 * (size_t)s);
-    else if constexpr (FMT == 2) return *reinterpret_cast<const unsigned *>(fb + 4 * (size_t)s);
-    else if constexpr (FMT == 3) return *reinterpret_cast<const float2 *>(fb + 8 * (size_t)s);
-    else {
-        const float *f = reinterpret_cast<const float *>(fb);
-        return make_float2(f[s], f[(size_t)n + s]);
-    }
-}
-
-// Raw word -> unscaled float pair; the converter scale (1/128, 1/32768) is
-// folded into the window table by the engine.  Bit-exact with the reference
-// LUTs: s8 b/128 (Signed8BitIQConverter.java:48-50), u8 (b-127.4f)/128
-// (Unsigned8BitIQConverter.java:48-50), s16 s/32768 (Signed16BitIQConverter.kt:52-55);
-// scaling by a power of two commutes with the fp32 rounding of the window multiply.
-template <int FMT>
-__device__ __forceinline__ float2 convert_raw(typename Raw<FMT>::T v) {
-    if constexpr (FMT == 0) return make_float2((float)(signed char)(v & 0xff), (float)(signed char)(v >> 8));
-    else if constexpr (FMT == 1) return make_float2((float)(v & 0xff) - 127.4f, (float)(v >> 8) - 127.4f);
-    else if constexpr (FMT == 2) return make_float2((float)(short)(v & 0xffff), (float)(short)(v >> 16));
-    else return v;
-}
-
-template <int FMT>
-__device__ __forceinline__ typename Raw<FMT>::T synth_raw(int s) {  // ablation input
-    if constexpr (FMT == 0 || FMT == 1) return (unsigned short)(s * 2654435761u >> 16);
-    else if constexpr (FMT == 2) return (unsigned)(s * 2654435761u);
-    else return make_float2((float)(s & 255) * 0.01f, (float)((s >> 3) & 255) * 0.01f);
-}
-
-__constant__ float2 kW8[8] = {{1.f, 0.f},          {kR2, -kR2}, {0.f, -1.f}, {-kR2, -kR2},
-                               {-1.f, 0.f},         {-kR2, kR2}, {0.f, 1.f},  {kR2, kR2}};
 
 // ----------------------------------------------------------------- main kernel
 // Persistent: each workgroup walks work items u = blockIdx.x + k*gridDim.x.
@@ -516,6 +351,7 @@ static hipError_t by_fmt(const FftLaunch &a) {
 }
 
 hipError_t launch_fft(const FftLaunch &a) {
+    if (a.variant != 1 && a.diag == 0 && a.max_logm == 14 && wide_supported(a.logn)) return launch_fft_wide(a);
     if (a.complex_out) {
         if (a.fmt != 3) return hipErrorInvalidValue;
         switch (a.logn) {  // complex output: f32 interleaved only

@@ -1,0 +1,353 @@
+// gfx950 "wide" sub-FFT kernel for M = 8192 / 16384: 256 threads, 64 points
+// per thread, two workgroups per CU.
+//
+// Why this shape (measured, DESIGN.md "Kernel design"): with one 1024-thread
+// workgroup per CU every wave runs the same phase between barriers, so HBM
+// loads, VALU butterflies, LDS exchanges and row stores never overlap and the
+// kernel time is their SUM.  Here each thread keeps 64 points in VGPRs
+// (256-VGPR budget at 2 waves/SIMD), an M-point FFT needs only two LDS
+// exchanges (radix 32,32,16 for 16K; 32,16,16 for 8K), and each exchange runs
+// in two half-rounds through an M/2 buffer, so a workgroup needs ~66 KiB of
+// LDS and two of them share a CU and interleave their phases.
+//
+// Per work item (frame, residue r) the pipeline is the same as the narrow
+// kernel (fft_kernels.hip): raw IQ -> LUT-exact convert -> window (fp32
+// multiply, NativeDsp.kt:55-58) [-> decimation-in-frequency pre-stage for
+// N = RS*M] -> FFT (sign -1, unscaled, natural order: pffft.h:117) ->
+// 10*log10(sqrt((Re/N)^2+(Im/N)^2)) + fft-shift (nativedsp.cpp:72-79) -> rows/ring.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "fft_common.h"
+#include "fft_kernels.h"
+
+namespace rfa {
+
+template <int LOGM>
+struct WGeo {
+    static constexpr int M = 1 << LOGM;
+    static constexpr int PT = 64;                // points per thread
+    static constexpr int TPF = M / PT;           // threads per sub-FFT
+    static constexpr int SLOTS = 256 / TPF;      // sub-FFTs per workgroup
+    static constexpr int THREADS = 256;
+    static constexpr int HALF = M / 2;           // exchange buffer (float2) per slot ...
+    static constexpr int HALFP = HALF + HALF / 32;  // ... with one float2 of padding per 32
+    static constexpr int R1 = LOGM == 14 ? 32 : 16;  // radix of pass 1 (pass 0: 32, pass 2: 16)
+    // LDS twiddle tables (float2), rows padded by one entry so that lanes
+    // reading different rows at the same column hit different banks:
+    // pass 1 [32][R1+1], pass 2 A,B [16][17]
+    static constexpr int P1_ROW = R1 + 1;
+    static constexpr int TW_P1 = 32 * P1_ROW;
+    static constexpr int P2_ROW = 17;
+    static constexpr int TW_P2 = 16 * P2_ROW;
+    static constexpr int TW_LDS = TW_P1 + 2 * TW_P2;
+};
+
+template <int Q, int LOGM>
+struct WPass {
+    using G = WGeo<LOGM>;
+    static constexpr int R = Q == 0 ? 32 : (Q == 1 ? G::R1 : 16);
+    static constexpr int P = Q == 0 ? 1 : (Q == 1 ? 32 : 32 * G::R1);  // product of earlier radices
+    static constexpr int NB = 64 / R;                                 // butterflies per thread
+    static constexpr int STRIDE = G::M / R;                           // input stride of a butterfly
+};
+
+// Padded exchange-buffer index (one float2 per 32): every access pattern of
+// the three passes is bank-conflict free, and because all lane
+// bases have zero low-5 bits w.r.t. the compile-time parts, pad(base + c) =
+// pad(base) + pad(c): LDS addresses are lane base + immediate.
+__device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
+
+// Exchange pass Q's outputs (v) for pass Q+1's inputs through the M/2 LDS
+// buffer in two half-rounds.  Round h moves the outputs of butterflies
+// [h*NB/2, (h+1)*NB/2) (they land in [h*M/2, (h+1)*M/2)) and the inputs with
+// t' in [h*R'/2, (h+1)*R'/2) (they come from the same half).  Reads go to fresh
+// SSA temporaries (compile-time renaming), so round-1 outputs are never
+// overwritten by round-0 inputs.
+template <int Q, int LOGM>
+__device__ __forceinline__ void exchange(float2 (&v)[64], float2 *buf, int tid) {
+    using G = WGeo<LOGM>;
+    using W = WPass<Q, LOGM>;
+    using N = WPass<Q + 1, LOGM>;
+    static_assert(W::NB >= 2 && N::R >= 2, "half-round split needs >= 2 butterflies and radix >= 2");
+    float2 in[2][32];
+    // lane bases (low 5 bits of every compile-time offset are zero)
+    const int wk = tid & (W::P - 1);
+    const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
+    const int rbase = padw(tid);                     // butterfly b adds TPF*b
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
+#pragma unroll
+            for (int t = 0; t < W::R; t++)
+                buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int b = 0; b < N::NB; b++) {
+#pragma unroll
+            for (int t = h * N::R / 2; t < (h + 1) * N::R / 2; t++)
+                in[h][b * (N::R / 2) + (t - h * N::R / 2)] =
+                    buf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
+        }
+        lds_barrier();
+    }
+#pragma unroll
+    for (int b = 0; b < N::NB; b++) {
+#pragma unroll
+        for (int t = 0; t < N::R; t++) {
+            const int h = t >= N::R / 2;
+            v[b * N::R + t] = in[h][b * (N::R / 2) + (t - h * N::R / 2)];
+        }
+    }
+}
+
+// Pass 1: k = tid & 31 is the same for every butterfly of the thread; its
+// twiddles W_{32 R}^{t k} sit contiguously at twp1[k][t] (exact, from double).
+template <int LOGM>
+__device__ __forceinline__ void pass1(float2 (&v)[64], int tid, const float2 *twp1) {
+    using W = WPass<1, LOGM>;
+    const float2 *row = twp1 + (tid & 31) * WGeo<LOGM>::P1_ROW;
+#pragma unroll
+    for (int t = 1; t < W::R; t++) {
+        const float2 w = row[t];
+#pragma unroll
+        for (int b = 0; b < W::NB; b++) v[b * W::R + t] = cmul(v[b * W::R + t], w);
+    }
+#pragma unroll
+    for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
+}
+
+// Pass 2 (last): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_64^{t b}
+// (M / TPF = 64); W_M^{t tid} = A[tid>>4][t] * B[tid&15][t] from two exact
+// 16x16 tables, the b-dependent factor is a compile-time constant.
+template <int T, int B>
+__device__ __forceinline__ void p2_const(float2 (&v)[64]) {
+    v[B * 16 + T] = w64<T * B>(v[B * 16 + T]);
+}
+template <int T>
+__device__ __forceinline__ void p2_const_t(float2 (&v)[64]) {
+    p2_const<T, 1>(v);
+    p2_const<T, 2>(v);
+    p2_const<T, 3>(v);
+}
+template <int... Ts>
+__device__ __forceinline__ void p2_const_all(float2 (&v)[64], std::integer_sequence<int, Ts...>) {
+    (p2_const_t<Ts>(v), ...);
+}
+
+template <int LOGM>
+__device__ __forceinline__ void pass2(float2 (&v)[64], int tid, const float2 *twp2) {
+    using W = WPass<2, LOGM>;
+    static_assert(W::R == 16 && W::NB == 4, "pass 2 layout");
+    constexpr int PR = WGeo<LOGM>::P2_ROW;
+    const float2 *ra = twp2 + (tid >> 4) * PR;
+    const float2 *rb = twp2 + WGeo<LOGM>::TW_P2 + (tid & 15) * PR;
+#pragma unroll
+    for (int t = 1; t < 16; t++) {
+        const float2 w = cmul(ra[t], rb[t]);
+#pragma unroll
+        for (int b = 0; b < 4; b++) v[b * 16 + t] = cmul(v[b * 16 + t], w);
+    }
+    p2_const_all(v, std::make_integer_sequence<int, 16>{});
+#pragma unroll
+    for (int b = 0; b < 4; b++) dft<16>(&v[b * 16]);
+}
+
+template <int LOGM, int RS, int FMT, bool COMPLEX_OUT>
+__global__ void __launch_bounds__(256, 2) fft_wide_kernel(FftLaunch a) {
+    using G = WGeo<LOGM>;
+    constexpr int M = G::M;
+    constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    constexpr int n = M * RS;
+    float2 *twp1 = lds;
+    float2 *twp2 = lds + G::TW_P1;
+    float2 *data = lds + G::TW_LDS;
+
+    for (int e = threadIdx.x; e < G::TW_LDS; e += G::THREADS) lds[e] = a.wide_tw[e];
+
+    // TPF >= 64: a wave never straddles slots, so slot (and hence every buffer
+    // descriptor below) is wave-uniform -- say so, or hipcc wraps each buffer
+    // access in a readfirstlane waterfall loop.
+    const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / G::TPF);
+    const int tid = threadIdx.x - slot * G::TPF;
+    float2 *buf = data + slot * G::HALFP;
+
+    int frame, r;
+    if constexpr (RS == 1) {
+        frame = blockIdx.x * G::SLOTS + slot;
+        r = 0;
+    } else {
+        // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
+        const int b = blockIdx.x;
+        const int g = b / (8 * RS), rem = b - g * (8 * RS);
+        r = rem >> 3;
+        frame = g * 8 + (rem & 7);
+    }
+    const bool active = frame < a.n_frames;
+    // inactive slots read zeros (num_records = 0) and store nothing
+    const rsrc_t in_rs = make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride,
+                                   active ? (unsigned)(n * BPS) : 0u);
+    const int planar_im = n * 4;
+    __syncthreads();
+
+    // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < 2, t < 32)
+    float2 v[64];
+    if constexpr (RS == 1) {
+        // all 64 raw samples of the thread in flight at once (buffer loads need
+        // no address registers), then the window (L2-resident) and convert.
+        const rsrc_t w_rs = make_rsrc(a.window, n * 4);
+        constexpr int SB = FMT == 4 ? 4 : BPS;
+        typename Raw<FMT>::T raw[64];
+#pragma unroll
+        for (int idx = 0; idx < 64; idx++) {
+            const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
+            raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
+        }
+#pragma unroll
+        for (int idx = 0; idx < 64; idx++) {
+            const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
+            const float w = buf_load_f32(w_rs, tid * 4, so * 4);
+            const float2 x = convert_raw<FMT>(raw[idx]);
+            v[idx] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
+        }
+    } else {
+        // y_r[m] = W_N^{m r} sum_j x[m + jM] w[m + jM] W_RS^{j r};  m = m' + 512 t, m' = tid + 256 b
+        // W_N^{m r} = pre_a[r][m'] * pre_b[r][t]
+        const rsrc_t w_rs = make_rsrc(a.window_il, n * 4);
+        const rsrc_t pa_rs = make_rsrc(a.wide_tw + G::TW_LDS, RS * 512 * 8);
+        const float2 *pre_b = a.wide_tw + G::TW_LDS + RS * 512 + r * 32;
+        float2 wr[RS];  // W_RS^{j r}: wave-uniform
+#pragma unroll
+        for (int j = 0; j < RS; j++) wr[j] = kW8[((j * r) * (8 / RS)) & 7];
+        float2 pa[2];
+#pragma unroll
+        for (int b = 0; b < 2; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + 256 * b) * 8, r * 512 * 8);
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int idx = c * 4 + q, b = idx >> 5, t = idx & 31;
+                const int mo = G::TPF * b + 512 * t;  // uniform part of m
+                float wj[RS];
+#pragma unroll
+                for (int j = 0; j < RS; j++) wj[j] = buf_load_f32(w_rs, tid * RS * 4, (mo * RS + j) * 4);
+                float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                for (int j = 0; j < RS; j++) {
+                    const float2 x = convert_raw<FMT>(
+                        buf_load_raw<FMT>(in_rs, tid * (FMT == 4 ? 4 : BPS), (mo + j * M) * (FMT == 4 ? 4 : BPS),
+                                          planar_im));
+                    const float2 xw = make_float2(x.x * wj[j], x.y * wj[j]);
+                    acc = (j == 0) ? xw : cadd(acc, cmul(xw, wr[j]));
+                }
+                v[idx] = (r == 0) ? acc : cmul(acc, cmul(pa[b], pre_b[t]));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+
+    // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
+#pragma unroll
+    for (int b = 0; b < 2; b++) dft<32>(&v[b * 32]);
+    exchange<0, LOGM>(v, buf, tid);
+    pass1<LOGM>(v, tid, twp1);
+    exchange<1, LOGM>(v, buf, tid);
+    pass2<LOGM>(v, tid, twp2);
+
+    if (!active) return;
+    // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
+    if constexpr (COMPLEX_OUT) {
+        const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * n, n * 8);
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+#pragma unroll
+            for (int t = 0; t < 16; t++)
+                buf_store_f32x2(v[b * 16 + t], o_rs, (RS * tid + r) * 8, RS * (G::TPF * b + t * (M / 16)) * 8);
+    } else {
+        constexpr float inv_n = 1.0f / (float)n;  // exact (power of two)
+        const bool to_ring = a.ring && frame >= a.ring_first;
+        int rr = 0;
+        if (to_ring) {
+            rr = (a.ring_base - frame) % a.ring_rows;
+            if (rr < 0) rr += a.ring_rows;
+        }
+        const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
+        const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
+        const int vo = (RS * tid + r) * 4;
+        // one uniform branch per item, not per store
+        auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+#pragma unroll
+                for (int t = 0; t < 16; t++) {
+                    const float2 x = v[b * 16 + t];
+                    const float re = x.x * inv_n, im = x.y * inv_n;
+                    const float db = db_from_power(re * re + im * im);  // nativedsp.cpp:73-78
+                    // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
+                    const int so = ((RS * (G::TPF * b + t * (M / 16)) + n / 2) & (n - 1)) * 4;
+                    buf_store_f32(db, rs0, vo, so);
+                    if constexpr (decltype(both)::value) buf_store_f32(db, rs1, vo, so);
+                }
+            }
+        };
+        if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
+        else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
+        else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+    }
+}
+
+template <int LOGM, int RS, int FMT, bool CO>
+static hipError_t launch_wide_one(const FftLaunch &a) {
+    using G = WGeo<LOGM>;
+    auto kern = &fft_wide_kernel<LOGM, RS, FMT, CO>;
+    const size_t lds = (size_t)(G::TW_LDS + G::SLOTS * G::HALFP) * sizeof(float2);
+    if (!a.wide_tw) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int blocks = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    if (blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
+    return hipGetLastError();
+}
+
+template <int LOGM, int RS, bool CO>
+static hipError_t wide_by_fmt(const FftLaunch &a) {
+    if constexpr (CO) {
+        return a.fmt == 3 ? launch_wide_one<LOGM, RS, 3, true>(a) : hipErrorInvalidValue;
+    } else {
+        switch (a.fmt) {
+        case 0: return launch_wide_one<LOGM, RS, 0, false>(a);
+        case 1: return launch_wide_one<LOGM, RS, 1, false>(a);
+        case 2: return launch_wide_one<LOGM, RS, 2, false>(a);
+        case 3: return launch_wide_one<LOGM, RS, 3, false>(a);
+        case 4: return launch_wide_one<LOGM, RS, 4, false>(a);
+        default: return hipErrorInvalidValue;
+        }
+    }
+}
+
+bool wide_supported(int logn) { return logn >= 13 && logn <= 17; }
+
+hipError_t launch_fft_wide(const FftLaunch &a) {
+    const bool co = a.complex_out != nullptr;
+    switch (a.logn) {
+    case 13: return co ? wide_by_fmt<13, 1, true>(a) : wide_by_fmt<13, 1, false>(a);
+    case 14: return co ? wide_by_fmt<14, 1, true>(a) : wide_by_fmt<14, 1, false>(a);
+    case 15: return co ? wide_by_fmt<14, 2, true>(a) : wide_by_fmt<14, 2, false>(a);
+    case 16: return co ? wide_by_fmt<14, 4, true>(a) : wide_by_fmt<14, 4, false>(a);
+    case 17: return co ? wide_by_fmt<14, 8, true>(a) : wide_by_fmt<14, 8, false>(a);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rfa

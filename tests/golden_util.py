@@ -17,13 +17,19 @@ import signals  # noqa: E402
 # north star: "output log-magnitude spectra match the reference CPU/nativedsp
 # path ... to within 0.01 dB with bit-exact bin ordering"
 DB_TOL = 0.01
-# The row unit is 10*log10(|X|/N) (a magnitude dB, nativedsp.cpp:78).  Bins
-# more than FLOOR_DB below the row's total (Parseval) level hold nothing but
-# fp32 rounding noise -- pffft's own rounding noise sits ~75 units below the
-# total and pffft leaves exact zeros where a float64 FFT has -300 dB -- so the
-# 0.01 dB bar is applied above that floor (>= 430x above the rounding noise,
-# i.e. <= 0.01 dB of relative error), and below it both sides must be deep.
+# The row unit is 10*log10(|X|/N) (a magnitude dB, nativedsp.cpp:78).  The
+# 0.01 dB bar is applied to bins above a floor below the row's total
+# (Parseval) level; below it a bin holds fp32 rounding noise (pffft leaves
+# exact zeros where a float64 FFT has -300 dB) and both sides only have to be
+# deep.  Two floors, because the reference is itself an fp32 FFT:
+#   vs the float64 oracle:   FLOOR_DB = 50 (magnitude 1e-5 of the total)
+#   vs pffft golden rows:    FLOOR_PFFFT_DB = 45
+# At 50 the reference's own pffft is 0.0077 dB off float64 on the s16/16K
+# fixture (tests/test_oracle.py measures it), so two correct fp32 FFTs can
+# differ by > 0.01 dB there; at 45 every bin is >= 1e4 x the fp32 rounding
+# noise and pffft-vs-float64 stays <= 0.0031 dB on every fixture.
 FLOOR_DB = 50.0
+FLOOR_PFFFT_DB = 45.0
 
 WINDOW_IDS = {"blackman": 0, "hann": 1, "none": 2}
 
@@ -67,8 +73,13 @@ def assert_same_peak_bins(got: np.ndarray, exp_argmax) -> None:
         assert row[a] >= row.max() - DB_TOL, (int(np.argmax(row)), a)
 
 
-def db_diff(got: np.ndarray, exp: np.ndarray) -> float:
-    """Max |dB difference| over bins within FLOOR_DB of the row's total level.
+def pffft_diff(got: np.ndarray, exp: np.ndarray) -> float:
+    """db_diff against rows produced by the reference's own pffft (see FLOOR_PFFFT_DB)."""
+    return db_diff(got, exp, FLOOR_PFFFT_DB)
+
+
+def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> float:
+    """Max |dB difference| over bins within floor_db (default FLOOR_DB) of the row's total level.
 
     Raises AssertionError on a structural mismatch: -inf vs finite above the
     floor, a NaN, or a deep bin on one side that is shallow on the other."""
@@ -76,6 +87,7 @@ def db_diff(got: np.ndarray, exp: np.ndarray) -> float:
     exp = np.atleast_2d(np.asarray(exp, np.float32))
     assert got.shape == exp.shape, (got.shape, exp.shape)
     assert not np.isnan(got).any(), "NaN in output"
+    floor = FLOOR_DB if floor_db is None else floor_db
     worst = 0.0
     for g, e in zip(got, exp):
         if np.all(np.isneginf(e)):
@@ -83,10 +95,10 @@ def db_diff(got: np.ndarray, exp: np.ndarray) -> float:
             continue
         mag = np.power(10.0, e.astype(np.float64) / 10.0)
         top = 10.0 * np.log10(np.sqrt(np.sum(mag * mag)))
-        live = e >= top - FLOOR_DB
+        live = e >= top - floor
         assert np.all(np.isfinite(g[live])), "non-finite bin above the floor"
         worst = max(worst, float(np.max(np.abs(g[live] - e[live]))))
         deep = ~live
         if deep.any():
-            assert np.all(g[deep] < top - FLOOR_DB + 20.0), "deep bin came out shallow"
+            assert np.all(g[deep] < top - floor + 20.0), "deep bin came out shallow"
     return worst
