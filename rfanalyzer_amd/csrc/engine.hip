@@ -33,6 +33,9 @@ struct rfa_handle {
     float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
     float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17)
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
+    int wide_pt = 32;                 // RFA_PT: wide-kernel points per thread
+    int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
+    long long stagger_ns = 0;         // RFA_STAGGER_NS
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     float2 *d_twc = nullptr, *d_twf = nullptr;
@@ -186,6 +189,9 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_fine = h->d_twf;
     a.tw_shift = h->tw_shift;
     a.diag = h->diag;
+    a.persist = h->persist;
+    a.wide_pt = h->wide_pt;
+    a.stagger_ns = h->stagger_ns;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
     if (a.window == h->d_window) a.window_il = h->d_window_il;
@@ -313,32 +319,17 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
     }
+    if (const char *d = std::getenv("RFA_PT")) h->wide_pt = std::atoi(d) == 64 ? 64 : 32;
     if (rfa::wide_supported(logn)) {
-        const int lm = logn == 13 ? 13 : 14, m = 1 << lm, rs = n / m, r1 = lm == 14 ? 32 : 16;
-        auto w = [](double num, double den) {  // exp(-2 pi i num/den), correctly rounded
-            const double a = -2.0 * M_PI * num / den;
-            return make_float2((float)std::cos(a), (float)std::sin(a));
-        };
-        std::vector<float2> blob;
-        // rows padded by one entry (bank-conflict-free LDS reads, fft_wide.hip WGeo)
-        for (int k = 0; k < 32; k++)
-            for (int t = 0; t <= r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
-        for (int th = 0; th < 16; th++)
-            for (int t = 0; t <= 16; t++) blob.push_back(w(16.0 * t * th, m));
-        for (int tl = 0; tl < 16; tl++)
-            for (int t = 0; t <= 16; t++) blob.push_back(w((double)t * tl, m));
-        if (rs > 1) {
-            for (int r = 0; r < rs; r++)
-                for (int mp = 0; mp < 512; mp++) blob.push_back(w((double)mp * r, n));
-            for (int r = 0; r < rs; r++)
-                for (int t = 0; t < 32; t++) blob.push_back(w(512.0 * t * r, n));
-        }
+        std::vector<float2> blob = rfa::wide_twiddles(logn, h->wide_pt);
         if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_wide_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
     }
     if (const char *d = std::getenv("RFA_KERNEL")) h->variant = std::string(d) == "narrow" ? 1 : 0;
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
+    if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
+    if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
     if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)

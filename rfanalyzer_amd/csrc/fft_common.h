@@ -17,11 +17,88 @@ namespace rfa {
 // ----------------------------------------------------------------- complex helpers
 RFA_HD float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 RFA_HD float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-RFA_HD float2 cmul(float2 a, float2 b) {
-    return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
-}
 RFA_HD float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * (-i)
 RFA_HD float2 mul_pi(float2 a) { return make_float2(-a.y, a.x); }  // * (+i)
+
+// ---- packed-fp32 complex arithmetic (gfx950 VOP3P).  A complex value is one
+// 64-bit VGPR pair; v_pk_add/mul/fma_f32 operate on both halves at once and
+// every source can be half-swapped (op_sel) and negated per half (neg_lo /
+// neg_hi) for free.  So a*(-i)^P + b*(-i)^Q is ONE instruction for any
+// quarter-turn rotations P, Q, and a complex multiply is two.  hipcc's own
+// packing of the float2 code needs extra v_mov for the swaps (checked on
+// hardware by scripts/pk_modifiers.hip).
+typedef float f2v __attribute__((ext_vector_type(2)));
+RFA_HD f2v to_v(float2 a) { return __builtin_bit_cast(f2v, a); }
+RFA_HD float2 from_v(f2v a) { return __builtin_bit_cast(float2, a); }
+
+template <int P>
+RFA_HD float2 rot(float2 a) {  // a * (-i)^P
+    constexpr int q = P & 3;
+    if constexpr (q == 0) return a;
+    else if constexpr (q == 1) return mul_mi(a);
+    else if constexpr (q == 2) return make_float2(-a.x, -a.y);
+    else return mul_pi(a);
+}
+
+// a * (-i)^P + b * (-i)^Q
+template <int P_, int Q_>
+RFA_HD float2 padd(float2 a_, float2 b_) {
+    constexpr int P = P_ & 3, Q = Q_ & 3;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (P == 0 && (Q == 0 || Q == 2)) {
+        return Q == 0 ? cadd(a_, b_) : csub(a_, b_);  // hipcc folds these itself
+    } else {
+        const f2v a = to_v(a_), b = to_v(b_);
+        f2v r;
+    if constexpr (P == 0 && Q == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 0 && Q == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 0 && Q == 2) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 0 && Q == 3) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 1 && Q == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 1 && Q == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 1 && Q == 2) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[0,1] neg_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 1 && Q == 3) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 2 && Q == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,1] neg_lo:[1,0] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 2 && Q == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[1,0] neg_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 2 && Q == 2) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,1] neg_lo:[1,1] neg_hi:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 2 && Q == 3) asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[1,1] neg_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 3 && Q == 0) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 3 && Q == 1) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 3 && Q == 2) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1] neg_lo:[1,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    else if constexpr (P == 3 && Q == 3) asm("v_pk_add_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,0] neg_lo:[1,1]" : "=v"(r) : "v"(a), "v"(b));
+        return from_v(r);
+    }
+#else
+    return cadd(rot<P>(a_), rot<Q>(b_));
+#endif
+}
+
+// complex a * w (w in a VGPR pair or an SGPR pair)
+RFA_HD float2 cmul(float2 a_, float2 w_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const f2v a = to_v(a_), w = to_v(w_);
+    f2v m, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(m) : "v"(a), "v"(w));  // (a.x w.x, a.x w.y)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a), "v"(w), "v"(m));  // (a.y (-w.y) + m.x, a.y w.x + m.y)
+    return from_v(r);
+#else
+    return make_float2(fmaf(a_.x, w_.x, -a_.y * w_.y), fmaf(a_.x, w_.y, a_.y * w_.x));
+#endif
+}
+// complex a * (c, s) for a compile-time constant (held in an SGPR pair)
+RFA_HD float2 cmulc(float2 a_, float c, float s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const f2v a = to_v(a_), w = {c, s};
+    f2v m, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(m) : "v"(a), "s"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a), "s"(w), "v"(m));
+    return from_v(r);
+#else
+    return make_float2(fmaf(a_.x, c, -a_.y * s), fmaf(a_.x, s, a_.y * c));
+#endif
+}
 
 // exp(-2*pi*i*m/16), correctly rounded fp32 constants.
 constexpr float kC1 = 0.923879532511286756f;  // cos(pi/8)
@@ -32,19 +109,15 @@ constexpr float kR2 = 0.707106781186547524f;  // sqrt(1/2)
 template <int m>
 RFA_HD float2 w16(float2 x) {
     constexpr int q = m & 15;
-    if constexpr (q == 0) return x;
-    else if constexpr (q == 4) return mul_mi(x);
-    else if constexpr (q == 8) return make_float2(-x.x, -x.y);
-    else if constexpr (q == 12) return mul_pi(x);
-    else if constexpr (q == 2) return make_float2((x.x + x.y) * kR2, (x.y - x.x) * kR2);
-    else if constexpr (q == 6) return make_float2((x.y - x.x) * kR2, -(x.x + x.y) * kR2);
-    else if constexpr (q == 10) return make_float2(-(x.x + x.y) * kR2, (x.x - x.y) * kR2);
-    else if constexpr (q == 14) return make_float2((x.x - x.y) * kR2, (x.x + x.y) * kR2);
-    else {
+    if constexpr ((q & 3) == 0) {
+        return rot<q / 4>(x);
+    } else if constexpr ((q & 3) == 2) {
+        // W_16^q = (-i)^((q-2)/4) * (1 - i)/sqrt(2):  x*(-i)^k + x*(-i)^(k+1), times sqrt(1/2)
+        return from_v(to_v(padd<(q - 2) / 4, (q + 2) / 4>(x, x)) * kR2);
+    } else {
         constexpr float c[16] = {1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1, 0, kS1, kR2, kC1};
         constexpr float s[16] = {0, kS1, kR2, kC1, 1, kC1, kR2, kS1, 0, -kS1, -kR2, -kC1, -1, -kC1, -kR2, -kS1};
-        // W = cos - i sin
-        return cmul(x, make_float2(c[q], -s[q]));
+        return cmulc(x, c[q], -s[q]);
     }
 }
 
@@ -54,13 +127,25 @@ RFA_HD void dft2(float2 &a, float2 &b) {
     a = cadd(t, b);
     b = csub(t, b);
 }
-RFA_HD void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
-    float2 s02 = cadd(x0, x2), d02 = csub(x0, x2), s13 = cadd(x1, x3), d13 = csub(x1, x3);
+// radix 2 with b pre-rotated by (-i)^P (folded into the adds)
+template <int P>
+RFA_HD void dft2r(float2 &a, float2 &b) {
+    const float2 t = a;
+    a = padd<0, P>(t, b);
+    b = padd<0, P + 2>(t, b);
+}
+// radix 4 with inputs x1, x2, x3 pre-rotated by (-i)^P1, (-i)^P2, (-i)^P3:
+// eight v_pk_add_f32 whatever the rotations.
+template <int P1, int P2, int P3>
+RFA_HD void dft4r(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
+    const float2 s02 = padd<0, P2>(x0, x2), d02 = padd<0, P2 + 2>(x0, x2);
+    const float2 s13 = padd<P1, P3>(x1, x3), d13 = padd<P1, P3 + 2>(x1, x3);
     x0 = cadd(s02, s13);
     x2 = csub(s02, s13);
-    x1 = cadd(d02, mul_mi(d13));
-    x3 = cadd(d02, mul_pi(d13));
+    x1 = padd<0, 1>(d02, d13);  // d02 - i d13
+    x3 = padd<0, 3>(d02, d13);  // d02 + i d13
 }
+RFA_HD void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) { dft4r<0, 0, 0>(x0, x1, x2, x3); }
 
 template <int R>
 RFA_HD void dft(float2 *u);
@@ -75,11 +160,10 @@ RFA_HD void dft<8>(float2 *u) {
     dft4(u[0], u[2], u[4], u[6]);
     dft4(u[1], u[3], u[5], u[7]);
     u[3] = w16<2>(u[3]);
-    u[5] = w16<4>(u[5]);
     u[7] = w16<6>(u[7]);
     dft2(u[0], u[1]);
     dft2(u[2], u[3]);
-    dft2(u[4], u[5]);
+    dft2r<1>(u[4], u[5]);  // u[5] * W_16^4 = -i u[5], folded
     dft2(u[6], u[7]);
     // position 2*q1 + q2 holds Y[q1 + 4 q2]
     float2 y[8];
@@ -88,10 +172,11 @@ RFA_HD void dft<8>(float2 *u) {
 #pragma unroll
     for (int q = 0; q < 8; q++) u[q] = y[q];
 }
-template <>
-RFA_HD void dft<16>(float2 *u) {
+// ROT8: input u[8] arrives pre-rotated by (-i)^ROT8 (folded into the first adds)
+template <int ROT8>
+RFA_HD void dft16r(float2 *u) {
     // t = 4*t1 + t2; DFT-4 over t1, twiddle W_16^{t2 q1}, DFT-4 over t2.
-    dft4(u[0], u[4], u[8], u[12]);
+    dft4r<0, ROT8, 0>(u[0], u[4], u[8], u[12]);
     dft4(u[1], u[5], u[9], u[13]);
     dft4(u[2], u[6], u[10], u[14]);
     dft4(u[3], u[7], u[11], u[15]);
@@ -99,14 +184,13 @@ RFA_HD void dft<16>(float2 *u) {
     u[6] = w16<2>(u[6]);
     u[7] = w16<3>(u[7]);
     u[9] = w16<2>(u[9]);
-    u[10] = w16<4>(u[10]);
     u[11] = w16<6>(u[11]);
     u[13] = w16<3>(u[13]);
     u[14] = w16<6>(u[14]);
     u[15] = w16<9>(u[15]);
     dft4(u[0], u[1], u[2], u[3]);
     dft4(u[4], u[5], u[6], u[7]);
-    dft4(u[8], u[9], u[10], u[11]);
+    dft4r<0, 1, 0>(u[8], u[9], u[10], u[11]);  // u[10] * W_16^4 = -i u[10], folded
     dft4(u[12], u[13], u[14], u[15]);
     // position 4*q1 + q2 holds Y[q1 + 4 q2]
     float2 y[16];
@@ -115,6 +199,8 @@ RFA_HD void dft<16>(float2 *u) {
 #pragma unroll
     for (int q = 0; q < 16; q++) u[q] = y[q];
 }
+template <>
+RFA_HD void dft<16>(float2 *u) { dft16r<0>(u); }
 
 // cos/sin(2*pi*m/64), correctly rounded fp32 (generated)
 constexpr float kCos64[64] = {1.0f, 0.99518472f, 0.980785251f, 0.956940353f, 0.923879504f, 0.881921291f, 0.831469595f, 0.773010433f, 0.707106769f, 0.634393275f, 0.555570245f, 0.471396744f, 0.382683426f, 0.290284663f, 0.195090324f, 0.0980171412f, 0.0f, -0.0980171412f, -0.195090324f, -0.290284663f, -0.382683426f, -0.471396744f, -0.555570245f, -0.634393275f, -0.707106769f, -0.773010433f, -0.831469595f, -0.881921291f, -0.923879504f, -0.956940353f, -0.980785251f, -0.99518472f, -1.0f, -0.99518472f, -0.980785251f, -0.956940353f, -0.923879504f, -0.881921291f, -0.831469595f, -0.773010433f, -0.707106769f, -0.634393275f, -0.555570245f, -0.471396744f, -0.382683426f, -0.290284663f, -0.195090324f, -0.0980171412f, 0.0f, 0.0980171412f, 0.195090324f, 0.290284663f, 0.382683426f, 0.471396744f, 0.555570245f, 0.634393275f, 0.707106769f, 0.773010433f, 0.831469595f, 0.881921291f, 0.923879504f, 0.956940353f, 0.980785251f, 0.99518472f};
@@ -125,7 +211,7 @@ template <int m>
 RFA_HD float2 w64(float2 x) {
     constexpr int q = m & 63;
     if constexpr ((q & 3) == 0) return w16<q / 4>(x);
-    else return cmul(x, make_float2(kCos64[q], -kSin64[q]));
+    else return cmulc(x, kCos64[q], -kSin64[q]);
 }
 
 template <>
@@ -134,11 +220,11 @@ RFA_HD void dft<32>(float2 *u) {
 #pragma unroll
     for (int t2 = 0; t2 < 16; t2++) dft2(u[t2], u[16 + t2]);
     u[17] = w64<2>(u[17]); u[18] = w64<4>(u[18]); u[19] = w64<6>(u[19]); u[20] = w64<8>(u[20]);
-    u[21] = w64<10>(u[21]); u[22] = w64<12>(u[22]); u[23] = w64<14>(u[23]); u[24] = w64<16>(u[24]);
+    u[21] = w64<10>(u[21]); u[22] = w64<12>(u[22]); u[23] = w64<14>(u[23]);
     u[25] = w64<18>(u[25]); u[26] = w64<20>(u[26]); u[27] = w64<22>(u[27]); u[28] = w64<24>(u[28]);
     u[29] = w64<26>(u[29]); u[30] = w64<28>(u[30]); u[31] = w64<30>(u[31]);
     dft<16>(u);
-    dft<16>(u + 16);
+    dft16r<1>(u + 16);  // u[24] * W_64^16 = -i u[24], folded
     // position 16*q1 + q2 holds Y[q1 + 2 q2]
     float2 y[32];
 #pragma unroll
@@ -288,13 +374,20 @@ __device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, i
     __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, soff, 0);
 }
 
-// 10*log10(sqrt(p)) (nativedsp.cpp:78) = (5*log10(2)) * log2(p) on the hardware
-// log2 (v_log_f32).  It flushes denormal inputs, so those are pre-scaled by
-// 2^24; log2(0) = -inf as in the reference.
-__device__ __forceinline__ float db_from_power(float p) {
-    const bool den = p < 1.17549435e-38f;
-    const float l = __builtin_amdgcn_logf(den ? p * 16777216.0f : p) - (den ? 24.0f : 0.0f);
-    return l * 1.50514997831990598f;
+// Row value 10*log10(sqrt((Re/N)^2 + (Im/N)^2)) (nativedsp.cpp:73-78) from the
+// UNSCALED FFT output x.  Scaling by 1/N is exact (power of two), so the power
+// is (x.x^2 + x.y^2) * 2^(-2 log2 N) and the dB value is
+// (5 log10 2) * (log2(x.x^2 + x.y^2) - 2 log2 N): one fma after the hardware
+// log2 (v_log_f32).  db_off = -(5 log10 2) * 2 log2 N.  Working unscaled keeps
+// the power 2^(2 log2 N) above the reference's, so it leaves the denormal range
+// (where v_log_f32 flushes) only for bins that are exactly or essentially zero
+// on both sides (-inf here, <= -380 dB in the reference).  log2(0) = -inf as
+// in the reference.
+constexpr float kDbPerLog2 = 1.50514997831990598f;  // 5*log10(2)
+RFA_HD float db_offset(int logn) { return -kDbPerLog2 * (float)(2 * logn); }
+__device__ __forceinline__ float db_unscaled(float2 x, float db_off) {
+    const float p = fmaf(x.x, x.x, x.y * x.y);
+    return fmaf(__builtin_amdgcn_logf(p), kDbPerLog2, db_off);
 }
 
 }  // namespace rfa

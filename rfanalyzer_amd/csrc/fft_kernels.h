@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 namespace rfa {
 
 // Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
@@ -36,6 +38,9 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    int wide_pt = 32;         // wide kernel points per thread (32 or 64; RFA_PT)
+    int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
+    long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
     int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
     int max_logm = 14;  // largest sub-FFT per workgroup (13 = experiment: 2 workgroups per CU)
     int diag = 0;  // ablation variant (profiling only): 1 no loads, 2 no stores, 4 no FFT passes
@@ -46,6 +51,7 @@ struct FftLaunch {
 hipError_t launch_fft(const FftLaunch &a);
 // The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
 bool wide_supported(int logn);
+std::vector<float2> wide_twiddles(int logn, int pt);
 hipError_t launch_fft_wide(const FftLaunch &a);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at

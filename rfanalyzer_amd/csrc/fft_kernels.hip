@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(Geo<LOGM>::THREADS, 4) fft_rows_kernel(FftLaun
                 }
             }
         } else {
-            const float inv_n = 1.0f / (float)n;  // exact (power of two)
+            const float db_off = db_offset(a.logn);
             float *row = a.rows ? a.rows + (size_t)frame * n : nullptr;
             float *ring = nullptr;
             if (a.ring && frame >= a.ring_first) {
@@ -270,9 +270,7 @@ __global__ void __launch_bounds__(Geo<LOGM>::THREADS, 4) fft_rows_kernel(FftLaun
                         const int ks = tid + b * G::TPF + t * PL::P;
                         const int kk = r + RS * ks;
                         const float2 x = v[b * PL::R + t];
-                        const float re = x.x * inv_n, im = x.y * inv_n;
-                        const float p = re * re + im * im;  // nativedsp.cpp:73-76
-                        const float db = 5.0f * log10f(p);   // == 10*log10(sqrt(p)), nativedsp.cpp:78
+                        const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
                         const int o = (kk + (n >> 1)) & (n - 1);  // fft-shift, nativedsp.cpp:77
                         dst[o] = db;
                         if (dst2) dst2[o] = db;
@@ -351,7 +349,7 @@ static hipError_t by_fmt(const FftLaunch &a) {
 }
 
 hipError_t launch_fft(const FftLaunch &a) {
-    if (a.variant != 1 && a.diag == 0 && a.max_logm == 14 && wide_supported(a.logn)) return launch_fft_wide(a);
+    if (a.variant != 1 && a.max_logm == 14 && wide_supported(a.logn)) return launch_fft_wide(a);
     if (a.complex_out) {
         if (a.fmt != 3) return hipErrorInvalidValue;
         switch (a.logn) {  // complex output: f32 interleaved only

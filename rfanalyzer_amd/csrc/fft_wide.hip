@@ -18,39 +18,42 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
+#include <vector>
 
 #include "fft_common.h"
 #include "fft_kernels.h"
 
 namespace rfa {
 
-template <int LOGM>
+template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
-    static constexpr int PT = 64;                // points per thread
-    static constexpr int TPF = M / PT;           // threads per sub-FFT
-    static constexpr int SLOTS = 256 / TPF;      // sub-FFTs per workgroup
-    static constexpr int THREADS = 256;
+    static constexpr int TPF = M / PT;           // threads per sub-FFT (PT points per thread)
+    static constexpr int THREADS = TPF < 256 ? 256 : TPF;
+    static constexpr int SLOTS = THREADS / TPF;  // sub-FFTs per workgroup
     static constexpr int HALF = M / 2;           // exchange buffer (float2) per slot ...
     static constexpr int HALFP = HALF + HALF / 32;  // ... with one float2 of padding per 32
     static constexpr int R1 = LOGM == 14 ? 32 : 16;  // radix of pass 1 (pass 0: 32, pass 2: 16)
-    // LDS twiddle tables (float2), rows padded by one entry so that lanes
-    // reading different rows at the same column hit different banks:
-    // pass 1 [32][R1+1], pass 2 A,B [16][17]
-    static constexpr int P1_ROW = R1 + 1;
+    // LDS twiddle tables (float2, t = 1..R-1 only).  Odd row strides (R-1)
+    // spread the rows read by one lane group over distinct banks.
+    static constexpr int P1_ROW = R1 - 1;        // pass 1: [k = tid & 31][t]
     static constexpr int TW_P1 = 32 * P1_ROW;
-    static constexpr int P2_ROW = 17;
-    static constexpr int TW_P2 = 16 * P2_ROW;
-    static constexpr int TW_LDS = TW_P1 + 2 * TW_P2;
+    static constexpr int LO = TPF > 256 ? 32 : 16;  // pass 2: tid = hi*LO + lo
+    static constexpr int P2_ROW = 15;
+    static constexpr int TW_P2A = (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
+    static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
+    static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
+    static constexpr int LDS_BYTES = (TW_LDS + SLOTS * HALFP) * 8;
 };
 
-template <int Q, int LOGM>
+template <int Q, int LOGM, int PT>
 struct WPass {
-    using G = WGeo<LOGM>;
+    using G = WGeo<LOGM, PT>;
     static constexpr int R = Q == 0 ? 32 : (Q == 1 ? G::R1 : 16);
     static constexpr int P = Q == 0 ? 1 : (Q == 1 ? 32 : 32 * G::R1);  // product of earlier radices
-    static constexpr int NB = 64 / R;                                 // butterflies per thread
+    static constexpr int NB = PT / R;                                 // butterflies per thread
     static constexpr int STRIDE = G::M / R;                           // input stride of a butterfly
 };
 
@@ -61,29 +64,37 @@ struct WPass {
 __device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
 
 // Exchange pass Q's outputs (v) for pass Q+1's inputs through the M/2 LDS
-// buffer in two half-rounds.  Round h moves the outputs of butterflies
-// [h*NB/2, (h+1)*NB/2) (they land in [h*M/2, (h+1)*M/2)) and the inputs with
-// t' in [h*R'/2, (h+1)*R'/2) (they come from the same half).  Reads go to fresh
-// SSA temporaries (compile-time renaming), so round-1 outputs are never
-// overwritten by round-0 inputs.
-template <int Q, int LOGM>
-__device__ __forceinline__ void exchange(float2 (&v)[64], float2 *buf, int tid) {
-    using G = WGeo<LOGM>;
-    using W = WPass<Q, LOGM>;
-    using N = WPass<Q + 1, LOGM>;
-    static_assert(W::NB >= 2 && N::R >= 2, "half-round split needs >= 2 butterflies and radix >= 2");
-    float2 in[2][32];
-    // lane bases (low 5 bits of every compile-time offset are zero)
+// buffer in two half-rounds.  Round h moves the outputs that land in
+// [h*M/2, (h+1)*M/2) -- butterflies [h*NB/2, (h+1)*NB/2), or, with one
+// butterfly per thread, the threads with (tid >= TPF/2) == h (wave-uniform) --
+// and the inputs with t' in [h*R'/2, (h+1)*R'/2), which come from the same
+// half.  Reads go to fresh SSA temporaries (compile-time renaming), so round-1
+// outputs are never overwritten by round-0 inputs.
+template <int Q, int LOGM, int PT>
+__device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
+    using G = WGeo<LOGM, PT>;
+    using W = WPass<Q, LOGM, PT>;
+    using N = WPass<Q + 1, LOGM, PT>;
+    static_assert(N::R >= 2, "half-round split needs radix >= 2");
+    float2 in[2][PT / 2];
     const int wk = tid & (W::P - 1);
     const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
     const int rbase = padw(tid);                     // butterfly b adds TPF*b
+    const int my_half = tid >= G::TPF / 2;           // NB == 1 writers only
 #pragma unroll
     for (int h = 0; h < 2; h++) {
+        if constexpr (W::NB == 1) {
+            if (my_half == h) {
 #pragma unroll
-        for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
+                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
+            }
+        } else {
 #pragma unroll
-            for (int t = 0; t < W::R; t++)
-                buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+            for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
+#pragma unroll
+                for (int t = 0; t < W::R; t++)
+                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+            }
         }
         lds_barrier();
 #pragma unroll
@@ -106,11 +117,11 @@ __device__ __forceinline__ void exchange(float2 (&v)[64], float2 *buf, int tid) 
 }
 
 // Pass 1: k = tid & 31 is the same for every butterfly of the thread; its
-// twiddles W_{32 R}^{t k} sit contiguously at twp1[k][t] (exact, from double).
-template <int LOGM>
-__device__ __forceinline__ void pass1(float2 (&v)[64], int tid, const float2 *twp1) {
-    using W = WPass<1, LOGM>;
-    const float2 *row = twp1 + (tid & 31) * WGeo<LOGM>::P1_ROW;
+// twiddles W_{32 R}^{t k} sit contiguously at twp1[k][t-1] (exact, from double).
+template <int LOGM, int PT>
+__device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *twp1) {
+    using W = WPass<1, LOGM, PT>;
+    const float2 *row = twp1 + (tid & 31) * WGeo<LOGM, PT>::P1_ROW - 1;
 #pragma unroll
     for (int t = 1; t < W::R; t++) {
         const float2 w = row[t];
@@ -121,45 +132,45 @@ __device__ __forceinline__ void pass1(float2 (&v)[64], int tid, const float2 *tw
     for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
 }
 
-// Pass 2 (last): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_64^{t b}
-// (M / TPF = 64); W_M^{t tid} = A[tid>>4][t] * B[tid&15][t] from two exact
-// 16x16 tables, the b-dependent factor is a compile-time constant.
-template <int T, int B>
-__device__ __forceinline__ void p2_const(float2 (&v)[64]) {
-    v[B * 16 + T] = w64<T * B>(v[B * 16 + T]);
+// Pass 2 (last): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_PT^{t b}
+// (M / TPF = PT); W_M^{t tid} = A[tid/LO][t] * B[tid%LO][t] from two exact
+// tables, the b-dependent factor is a compile-time constant.
+template <int PT, int T, int B>
+__device__ __forceinline__ void p2_const(float2 (&v)[PT]) {
+    v[B * 16 + T] = w64<T * B * (64 / PT)>(v[B * 16 + T]);
 }
-template <int T>
-__device__ __forceinline__ void p2_const_t(float2 (&v)[64]) {
-    p2_const<T, 1>(v);
-    p2_const<T, 2>(v);
-    p2_const<T, 3>(v);
+template <int PT, int T, int... Bs>
+__device__ __forceinline__ void p2_const_t(float2 (&v)[PT], std::integer_sequence<int, Bs...>) {
+    (p2_const<PT, T, Bs + 1>(v), ...);
 }
-template <int... Ts>
-__device__ __forceinline__ void p2_const_all(float2 (&v)[64], std::integer_sequence<int, Ts...>) {
-    (p2_const_t<Ts>(v), ...);
+template <int PT, int... Ts>
+__device__ __forceinline__ void p2_const_all(float2 (&v)[PT], std::integer_sequence<int, Ts...>) {
+    (p2_const_t<PT, Ts>(v, std::make_integer_sequence<int, PT / 16 - 1>{}), ...);
 }
 
-template <int LOGM>
-__device__ __forceinline__ void pass2(float2 (&v)[64], int tid, const float2 *twp2) {
-    using W = WPass<2, LOGM>;
-    static_assert(W::R == 16 && W::NB == 4, "pass 2 layout");
-    constexpr int PR = WGeo<LOGM>::P2_ROW;
-    const float2 *ra = twp2 + (tid >> 4) * PR;
-    const float2 *rb = twp2 + WGeo<LOGM>::TW_P2 + (tid & 15) * PR;
+template <int LOGM, int PT>
+__device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *twp2) {
+    using G = WGeo<LOGM, PT>;
+    using W = WPass<2, LOGM, PT>;
+    static_assert(W::R == 16, "pass 2 layout");
+    const float2 *ra = twp2 + (tid / G::LO) * G::P2_ROW - 1;
+    const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
 #pragma unroll
     for (int t = 1; t < 16; t++) {
         const float2 w = cmul(ra[t], rb[t]);
 #pragma unroll
-        for (int b = 0; b < 4; b++) v[b * 16 + t] = cmul(v[b * 16 + t], w);
+        for (int b = 0; b < W::NB; b++) v[b * 16 + t] = cmul(v[b * 16 + t], w);
     }
-    p2_const_all(v, std::make_integer_sequence<int, 16>{});
+    p2_const_all<PT>(v, std::make_integer_sequence<int, 16>{});
 #pragma unroll
-    for (int b = 0; b < 4; b++) dft<16>(&v[b * 16]);
+    for (int b = 0; b < W::NB; b++) dft<16>(&v[b * 16]);
 }
 
-template <int LOGM, int RS, int FMT, bool COMPLEX_OUT>
-__global__ void __launch_bounds__(256, 2) fft_wide_kernel(FftLaunch a) {
-    using G = WGeo<LOGM>;
+// DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
+// 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
+template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0>
+__global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) fft_wide_kernel(FftLaunch a) {
+    using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -177,135 +188,163 @@ __global__ void __launch_bounds__(256, 2) fft_wide_kernel(FftLaunch a) {
     const int tid = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::HALFP;
 
-    int frame, r;
-    if constexpr (RS == 1) {
-        frame = blockIdx.x * G::SLOTS + slot;
-        r = 0;
-    } else {
-        // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
-        const int b = blockIdx.x;
-        const int g = b / (8 * RS), rem = b - g * (8 * RS);
-        r = rem >> 3;
-        frame = g * 8 + (rem & 7);
-    }
-    const bool active = frame < a.n_frames;
-    // inactive slots read zeros (num_records = 0) and store nothing
-    const rsrc_t in_rs = make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride,
-                                   active ? (unsigned)(n * BPS) : 0u);
-    const int planar_im = n * 4;
-    __syncthreads();
+    const int items = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    __syncthreads();  // twiddle tables in LDS
 
-    // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < 2, t < 32)
-    float2 v[64];
-    if constexpr (RS == 1) {
-        // all 64 raw samples of the thread in flight at once (buffer loads need
-        // no address registers), then the window (L2-resident) and convert.
-        const rsrc_t w_rs = make_rsrc(a.window, n * 4);
-        constexpr int SB = FMT == 4 ? 4 : BPS;
-        typename Raw<FMT>::T raw[64];
-#pragma unroll
-        for (int idx = 0; idx < 64; idx++) {
-            const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
-            raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
+    // One work item (SLOTS frames, or one residue of a frame).  Between items no
+    // extra barrier is needed: the last LDS reads of an item (exchange 1) are
+    // followed by a barrier before anyone leaves the FFT.
+    auto body = [&](int u) {
+        // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
+        // reads out of the item loop, which would need ~90 more VGPRs
+        int z;
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
+        int frame, r;
+        if constexpr (RS == 1) {
+            frame = u * G::SLOTS + slot;
+            r = 0;
+        } else {
+            // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
+            const int g = u / (8 * RS), rem = u - g * (8 * RS);
+            r = rem >> 3;
+            frame = g * 8 + (rem & 7);
         }
-#pragma unroll
-        for (int idx = 0; idx < 64; idx++) {
-            const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
-            const float w = buf_load_f32(w_rs, tid * 4, so * 4);
-            const float2 x = convert_raw<FMT>(raw[idx]);
-            v[idx] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
-        }
-    } else {
-        // y_r[m] = W_N^{m r} sum_j x[m + jM] w[m + jM] W_RS^{j r};  m = m' + 512 t, m' = tid + 256 b
-        // W_N^{m r} = pre_a[r][m'] * pre_b[r][t]
-        const rsrc_t w_rs = make_rsrc(a.window_il, n * 4);
-        const rsrc_t pa_rs = make_rsrc(a.wide_tw + G::TW_LDS, RS * 512 * 8);
-        const float2 *pre_b = a.wide_tw + G::TW_LDS + RS * 512 + r * 32;
-        float2 wr[RS];  // W_RS^{j r}: wave-uniform
-#pragma unroll
-        for (int j = 0; j < RS; j++) wr[j] = kW8[((j * r) * (8 / RS)) & 7];
-        float2 pa[2];
-#pragma unroll
-        for (int b = 0; b < 2; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + 256 * b) * 8, r * 512 * 8);
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int idx = c * 4 + q, b = idx >> 5, t = idx & 31;
-                const int mo = G::TPF * b + 512 * t;  // uniform part of m
-                float wj[RS];
-#pragma unroll
-                for (int j = 0; j < RS; j++) wj[j] = buf_load_f32(w_rs, tid * RS * 4, (mo * RS + j) * 4);
-                float2 acc = make_float2(0.f, 0.f);
-#pragma unroll
-                for (int j = 0; j < RS; j++) {
-                    const float2 x = convert_raw<FMT>(
-                        buf_load_raw<FMT>(in_rs, tid * (FMT == 4 ? 4 : BPS), (mo + j * M) * (FMT == 4 ? 4 : BPS),
-                                          planar_im));
-                    const float2 xw = make_float2(x.x * wj[j], x.y * wj[j]);
-                    acc = (j == 0) ? xw : cadd(acc, cmul(xw, wr[j]));
-                }
-                v[idx] = (r == 0) ? acc : cmul(acc, cmul(pa[b], pre_b[t]));
+        const bool active = frame < a.n_frames;
+        // inactive slots read zeros (num_records = 0) and store nothing
+        const rsrc_t in_rs = make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride,
+                                       active ? (unsigned)(n * BPS) : 0u);
+        const int planar_im = n * 4;
+
+        // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
+        float2 v[PT];
+        if constexpr (RS == 1) {
+            // all PT raw samples of the thread in flight at once (buffer loads need
+            // no address registers), then the window (L2-resident) and convert.
+            const rsrc_t w_rs = make_rsrc(a.window, n * 4);
+            constexpr int SB = FMT == 4 ? 4 : BPS;
+            typename Raw<FMT>::T raw[PT];
+    #pragma unroll
+            for (int idx = 0; idx < PT; idx++) {
+                const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
+                if constexpr (DIAG & 1) raw[idx] = synth_raw<FMT>(so + tid);
+                else raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
             }
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-
-    // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
-#pragma unroll
-    for (int b = 0; b < 2; b++) dft<32>(&v[b * 32]);
-    exchange<0, LOGM>(v, buf, tid);
-    pass1<LOGM>(v, tid, twp1);
-    exchange<1, LOGM>(v, buf, tid);
-    pass2<LOGM>(v, tid, twp2);
-
-    if (!active) return;
-    // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
-    if constexpr (COMPLEX_OUT) {
-        const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * n, n * 8);
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-#pragma unroll
-            for (int t = 0; t < 16; t++)
-                buf_store_f32x2(v[b * 16 + t], o_rs, (RS * tid + r) * 8, RS * (G::TPF * b + t * (M / 16)) * 8);
-    } else {
-        constexpr float inv_n = 1.0f / (float)n;  // exact (power of two)
-        const bool to_ring = a.ring && frame >= a.ring_first;
-        int rr = 0;
-        if (to_ring) {
-            rr = (a.ring_base - frame) % a.ring_rows;
-            if (rr < 0) rr += a.ring_rows;
-        }
-        const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
-        const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
-        const int vo = (RS * tid + r) * 4;
-        // one uniform branch per item, not per store
-        auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-#pragma unroll
-                for (int t = 0; t < 16; t++) {
-                    const float2 x = v[b * 16 + t];
-                    const float re = x.x * inv_n, im = x.y * inv_n;
-                    const float db = db_from_power(re * re + im * im);  // nativedsp.cpp:73-78
-                    // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
-                    const int so = ((RS * (G::TPF * b + t * (M / 16)) + n / 2) & (n - 1)) * 4;
-                    buf_store_f32(db, rs0, vo, so);
-                    if constexpr (decltype(both)::value) buf_store_f32(db, rs1, vo, so);
-                }
+    #pragma unroll
+            for (int idx = 0; idx < PT; idx++) {
+                const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
+                const float w = (DIAG & 16) ? 1.0f : buf_load_f32(w_rs, tid * 4, so * 4);
+                const float2 x = convert_raw<FMT>(raw[idx]);
+                v[idx] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
             }
-        };
-        if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
-        else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
-        else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+        } else {
+            // y_r[m] = W_N^{m r} sum_j x[m + jM] w[m + jM] W_RS^{j r};  m = m' + (M/32) t, m' = tid + TPF b
+            // W_N^{m r} = pre_a[r][m'] * pre_b[r][t]
+            const rsrc_t w_rs = make_rsrc(a.window_il, n * 4);
+            const rsrc_t pa_rs = make_rsrc(a.wide_tw + G::TW_LDS, RS * (M / 32) * 8);
+            const float2 *pre_b = a.wide_tw + G::TW_LDS + RS * (M / 32) + r * 32;
+            float2 wr[RS];  // W_RS^{j r}: wave-uniform
+    #pragma unroll
+            for (int j = 0; j < RS; j++) wr[j] = kW8[((j * r) * (8 / RS)) & 7];
+            float2 pa[PT / 32];
+    #pragma unroll
+            for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, r * (M / 32) * 8);
+    #pragma unroll
+            for (int c = 0; c < PT / 4; c++) {
+    #pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int idx = c * 4 + q, b = idx >> 5, t = idx & 31;
+                    const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
+                    float wj[RS];
+    #pragma unroll
+                    for (int j = 0; j < RS; j++) wj[j] = buf_load_f32(w_rs, tid * RS * 4, (mo * RS + j) * 4);
+                    float2 acc = make_float2(0.f, 0.f);
+    #pragma unroll
+                    for (int j = 0; j < RS; j++) {
+                        const float2 x = convert_raw<FMT>(
+                            buf_load_raw<FMT>(in_rs, tid * (FMT == 4 ? 4 : BPS), (mo + j * M) * (FMT == 4 ? 4 : BPS),
+                                              planar_im));
+                        const float2 xw = make_float2(x.x * wj[j], x.y * wj[j]);
+                        acc = (j == 0) ? xw : cadd(acc, cmul(xw, wr[j]));
+                    }
+                    v[idx] = (r == 0) ? acc : cmul(acc, cmul(pa[b], pre_b[t]));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+        // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
+    #pragma unroll
+        for (int b = 0; b < PT / 32; b++)
+            if constexpr (!(DIAG & 4)) dft<32>(&v[b * 32]);
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT>(v, buf, tid);
+        if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
+        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT>(v, buf, tid);
+        if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
+        if constexpr ((DIAG & 12) != 0) {
+    #pragma unroll
+            for (int q = 0; q < PT; q++) asm volatile("" : "+v"(v[q].x), "+v"(v[q].y));
+        }
+
+        if (!active) return;
+        // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
+        if constexpr (COMPLEX_OUT) {
+            const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * n, n * 8);
+    #pragma unroll
+            for (int b = 0; b < PT / 16; b++)
+    #pragma unroll
+                for (int t = 0; t < 16; t++)
+                    buf_store_f32x2(v[b * 16 + t], o_rs, (RS * tid + r) * 8, RS * (G::TPF * b + t * (M / 16)) * 8);
+        } else {
+            constexpr float db_off = -kDbPerLog2 * (float)(2 * (LOGM + (RS == 1 ? 0 : RS == 2 ? 1 : RS == 4 ? 2 : 3)));
+            const bool to_ring = a.ring && frame >= a.ring_first;
+            int rr = 0;
+            if (to_ring) {
+                rr = (a.ring_base - frame) % a.ring_rows;
+                if (rr < 0) rr += a.ring_rows;
+            }
+            const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
+            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
+            const int vo = (RS * tid + r) * 4;
+            // one uniform branch per item, not per store
+            auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
+    #pragma unroll
+                for (int b = 0; b < PT / 16; b++) {
+    #pragma unroll
+                    for (int t = 0; t < 16; t++) {
+                        const float2 x = v[b * 16 + t];
+                        const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
+                        // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
+                        const int so = ((RS * (G::TPF * b + t * (M / 16)) + n / 2) & (n - 1)) * 4;
+                        if constexpr (DIAG & 2) {
+                            asm volatile("" ::"v"(db));
+                        } else {
+                            buf_store_f32(db, rs0, vo, so);
+                            if constexpr (decltype(both)::value) buf_store_f32(db, rs1, vo, so);
+                        }
+                    }
+                }
+            };
+            if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
+            else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
+            else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+        }
+    };
+    if (a.stagger_ns > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
+        // persistent grid: the second resident workgroup of a CU starts late so the
+        // two interleave memory and compute phases (speed only; RFA_STAGGER_NS)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
+            __builtin_amdgcn_s_sleep(32);
     }
+    for (int u = blockIdx.x; u < items; u += gridDim.x) body(u);
 }
 
-template <int LOGM, int RS, int FMT, bool CO>
+template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0>
 static hipError_t launch_wide_one(const FftLaunch &a) {
-    using G = WGeo<LOGM>;
-    auto kern = &fft_wide_kernel<LOGM, RS, FMT, CO>;
-    const size_t lds = (size_t)(G::TW_LDS + G::SLOTS * G::HALFP) * sizeof(float2);
+    using G = WGeo<LOGM, PT>;
+    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG>;
+    const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
@@ -314,23 +353,33 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int blocks = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
-    if (blocks <= 0) return hipSuccess;
+    const int items = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    if (items <= 0) return hipSuccess;
+    int blocks = items;
+    if (a.persist > 0) {  // persistent: a.persist workgroups per CU (grid a multiple of 8*RS)
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+        }
+        blocks = std::min(items, cus * a.persist);
+    }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
     return hipGetLastError();
 }
 
-template <int LOGM, int RS, bool CO>
+template <int LOGM, int PT, int RS, bool CO>
 static hipError_t wide_by_fmt(const FftLaunch &a) {
     if constexpr (CO) {
-        return a.fmt == 3 ? launch_wide_one<LOGM, RS, 3, true>(a) : hipErrorInvalidValue;
+        return a.fmt == 3 ? launch_wide_one<LOGM, PT, RS, 3, true>(a) : hipErrorInvalidValue;
     } else {
         switch (a.fmt) {
-        case 0: return launch_wide_one<LOGM, RS, 0, false>(a);
-        case 1: return launch_wide_one<LOGM, RS, 1, false>(a);
-        case 2: return launch_wide_one<LOGM, RS, 2, false>(a);
-        case 3: return launch_wide_one<LOGM, RS, 3, false>(a);
-        case 4: return launch_wide_one<LOGM, RS, 4, false>(a);
+        case 0: return launch_wide_one<LOGM, PT, RS, 0, false>(a);
+        case 1: return launch_wide_one<LOGM, PT, RS, 1, false>(a);
+        case 2: return launch_wide_one<LOGM, PT, RS, 2, false>(a);
+        case 3: return launch_wide_one<LOGM, PT, RS, 3, false>(a);
+        case 4: return launch_wide_one<LOGM, PT, RS, 4, false>(a);
         default: return hipErrorInvalidValue;
         }
     }
@@ -338,14 +387,64 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
 
 bool wide_supported(int logn) { return logn >= 13 && logn <= 17; }
 
+// Twiddle blob for the wide kernel (layout must match WGeo): pass-1 [32][R1-1],
+// pass-2 A [TPF/LO][15], B [LO][15], pre-stage pre_a [RS][M/32], pre_b [RS][32].
+std::vector<float2> wide_twiddles(int logn, int pt) {
+    const int lm = logn == 13 ? 13 : 14, m = 1 << lm, n = 1 << logn, rs = n / m;
+    const int r1 = lm == 14 ? 32 : 16, tpf = m / pt, lo = tpf > 256 ? 32 : 16;
+    auto w = [](double num, double den) {  // exp(-2 pi i num/den), correctly rounded from double
+        const double a = -2.0 * M_PI * num / den;
+        return make_float2((float)std::cos(a), (float)std::sin(a));
+    };
+    std::vector<float2> blob;
+    for (int k = 0; k < 32; k++)
+        for (int t = 1; t < r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
+    for (int hi = 0; hi < tpf / lo; hi++)
+        for (int t = 1; t < 16; t++) blob.push_back(w((double)t * hi * lo, m));
+    for (int l = 0; l < lo; l++)
+        for (int t = 1; t < 16; t++) blob.push_back(w((double)t * l, m));
+    if (rs > 1) {
+        for (int r = 0; r < rs; r++)
+            for (int mp = 0; mp < m / 32; mp++) blob.push_back(w((double)mp * r, n));
+        for (int r = 0; r < rs; r++)
+            for (int t = 0; t < 32; t++) blob.push_back(w((double)(m / 32) * t * r, n));
+    }
+    return blob;
+}
+
 hipError_t launch_fft_wide(const FftLaunch &a) {
     const bool co = a.complex_out != nullptr;
+    if (a.diag) {  // ablations: 16K, s8 only
+        if (a.logn != 14 || a.fmt != 0 || co) return hipErrorInvalidValue;
+        switch (a.diag) {
+        case 1: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 1>(a) : launch_wide_one<14, 32, 1, 0, false, 1>(a));
+        case 2: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 2>(a) : launch_wide_one<14, 32, 1, 0, false, 2>(a));
+        case 3: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 3>(a) : launch_wide_one<14, 32, 1, 0, false, 3>(a));
+        case 4: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 4>(a) : launch_wide_one<14, 32, 1, 0, false, 4>(a));
+        case 8: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 8>(a) : launch_wide_one<14, 32, 1, 0, false, 8>(a));
+        case 12: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 12>(a) : launch_wide_one<14, 32, 1, 0, false, 12>(a));
+        case 16: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 16>(a) : launch_wide_one<14, 32, 1, 0, false, 16>(a));
+        case 19: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 19>(a) : launch_wide_one<14, 32, 1, 0, false, 19>(a));
+        case 31: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 31>(a) : launch_wide_one<14, 32, 1, 0, false, 31>(a));
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (a.wide_pt == 64) {
+        switch (a.logn) {
+        case 13: return co ? wide_by_fmt<13, 64, 1, true>(a) : wide_by_fmt<13, 64, 1, false>(a);
+        case 14: return co ? wide_by_fmt<14, 64, 1, true>(a) : wide_by_fmt<14, 64, 1, false>(a);
+        case 15: return co ? wide_by_fmt<14, 64, 2, true>(a) : wide_by_fmt<14, 64, 2, false>(a);
+        case 16: return co ? wide_by_fmt<14, 64, 4, true>(a) : wide_by_fmt<14, 64, 4, false>(a);
+        case 17: return co ? wide_by_fmt<14, 64, 8, true>(a) : wide_by_fmt<14, 64, 8, false>(a);
+        default: return hipErrorInvalidValue;
+        }
+    }
     switch (a.logn) {
-    case 13: return co ? wide_by_fmt<13, 1, true>(a) : wide_by_fmt<13, 1, false>(a);
-    case 14: return co ? wide_by_fmt<14, 1, true>(a) : wide_by_fmt<14, 1, false>(a);
-    case 15: return co ? wide_by_fmt<14, 2, true>(a) : wide_by_fmt<14, 2, false>(a);
-    case 16: return co ? wide_by_fmt<14, 4, true>(a) : wide_by_fmt<14, 4, false>(a);
-    case 17: return co ? wide_by_fmt<14, 8, true>(a) : wide_by_fmt<14, 8, false>(a);
+    case 13: return co ? wide_by_fmt<13, 32, 1, true>(a) : wide_by_fmt<13, 32, 1, false>(a);
+    case 14: return co ? wide_by_fmt<14, 32, 1, true>(a) : wide_by_fmt<14, 32, 1, false>(a);
+    case 15: return co ? wide_by_fmt<14, 32, 2, true>(a) : wide_by_fmt<14, 32, 2, false>(a);
+    case 16: return co ? wide_by_fmt<14, 32, 4, true>(a) : wide_by_fmt<14, 32, 4, false>(a);
+    case 17: return co ? wide_by_fmt<14, 32, 8, true>(a) : wide_by_fmt<14, 32, 8, false>(a);
     default: return hipErrorInvalidValue;
     }
 }
