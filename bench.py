@@ -208,7 +208,7 @@ def main():
                    "parallelism": f"streams{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": "fft_rows_kernel", "kernel_ms": round(kernel_ms, 4),
+                     "kernel": eng.main_kernel_name(), "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

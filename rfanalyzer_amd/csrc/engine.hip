@@ -33,7 +33,6 @@ struct rfa_handle {
     float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
     float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17)
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
-    int wide_pt = 32;                 // RFA_PT: wide-kernel points per thread
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
@@ -46,6 +45,8 @@ struct rfa_handle {
     bool have_rows = false;  // at least one row pushed since the last reset
     float *d_peaks = nullptr;
     float *d_ema = nullptr;
+    float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
+    int state_chunks = 1;
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     int64_t last_frequency = 0, last_sample_rate = 0;
@@ -190,7 +191,6 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_shift = h->tw_shift;
     a.diag = h->diag;
     a.persist = h->persist;
-    a.wide_pt = h->wide_pt;
     a.stagger_ns = h->stagger_ns;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
@@ -319,9 +319,8 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
     }
-    if (const char *d = std::getenv("RFA_PT")) h->wide_pt = std::atoi(d) == 64 ? 64 : 32;
     if (rfa::wide_supported(logn)) {
-        std::vector<float2> blob = rfa::wide_twiddles(logn, h->wide_pt);
+        std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT);
         if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_wide_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
@@ -356,6 +355,13 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     }
     if (cfg->peak_hold && hipMalloc(&h->d_peaks, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (cfg->avg_mode == RFA_AVG_EMA && hipMalloc(&h->d_ema, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+    if (h->d_peaks || h->d_ema) {
+        // enough (bin, chunk) threads to fill the chip (~2^19) for large batches
+        h->state_chunks = (int)std::min<size_t>(32, std::max<size_t>(1, ((size_t)1 << 19) / n));
+        if (h->state_chunks > 1 &&
+            hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
+            return bail(RFA_ERR_NOMEM);
+    }
     if (hipMalloc(&h->d_boxcar, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (clear_ring(h) || reset_peaks_ema(h)) return bail(RFA_ERR_HIP);
     if (hipStreamSynchronize(h->stream) != hipSuccess) return bail(RFA_ERR_HIP);
@@ -380,6 +386,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_ring_tmp);
     hipFree(h->d_peaks);
     hipFree(h->d_ema);
+    hipFree(h->d_state_part);
     hipFree(h->d_boxcar);
     hipFree(h->d_in);
     hipFree(h->d_rows);
@@ -469,6 +476,8 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         s.peaks = h->d_peaks;
         s.ema = h->d_ema;
         s.ema_alpha = h->cfg.ema_alpha;
+        s.part = h->d_state_part;
+        s.max_chunks = h->state_chunks;
         s.stream = h->stream;
         if (rows_in_ring) {
             s.rows = h->d_ring;
@@ -695,6 +704,12 @@ int rfa_set_profiling(rfa_handle *h, int enable) {
     if (!enable && h->profile) drain_events(h, true);
     h->profile = enable != 0;
     return RFA_OK;
+}
+
+const char *rfa_main_kernel_name(const rfa_handle *h) {
+    if (!h) return "";
+    const bool wide = h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(h->logn);
+    return wide ? "fft_wide_kernel" : "fft_rows_kernel";
 }
 
 int rfa_get_kernel_time(rfa_handle *h, double *total_ms, int64_t *launches) {

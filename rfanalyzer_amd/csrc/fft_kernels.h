@@ -38,7 +38,6 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
-    int wide_pt = 32;         // wide kernel points per thread (32 or 64; RFA_PT)
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
     int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
@@ -51,6 +50,7 @@ struct FftLaunch {
 hipError_t launch_fft(const FftLaunch &a);
 // The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
 bool wide_supported(int logn);
+constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
 std::vector<float2> wide_twiddles(int logn, int pt);
 hipError_t launch_fft_wide(const FftLaunch &a);
 
@@ -67,6 +67,8 @@ struct StateLaunch {
     float *peaks = nullptr;  // may be null
     float *ema = nullptr;    // may be null; -inf = uninitialised
     float ema_alpha = 0.f;
+    float4 *part = nullptr;  // chunk summaries [max_chunks][n] (null: sequential kernel only)
+    int max_chunks = 1;
     hipStream_t stream = nullptr;
 };
 hipError_t launch_state(const StateLaunch &a);

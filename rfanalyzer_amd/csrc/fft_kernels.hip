@@ -389,23 +389,69 @@ hipError_t launch_fft(const FftLaunch &a) {
 // ----------------------------------------------------------------- state / ring kernels
 // Peak-hold (FftProcessor.kt:241-242) and EMA (extension; GlobalPerformanceData.kt:44-50
 // idiom, -inf/uninitialised state re-seeded by the next frame), frame by frame.
+__device__ __forceinline__ const float *state_row(const StateLaunch &a, int f) {
+    if (a.ring_rows > 0) {
+        int rr = (a.ring_base - f) % a.ring_rows;
+        return a.rows + (size_t)(rr < 0 ? rr + a.ring_rows : rr) * a.n;
+    }
+    return a.rows + (size_t)((long long)f * a.row_stride);
+}
+
+// Sequential peak-hold / EMA over the batch (one thread per bin, frames in order).
+// Peak: FftProcessor.kt:229-232.  EMA (extension): em += alpha (x - em); an
+// uninitialised (-inf) average takes the frame's value.
 __global__ void state_kernel(StateLaunch a) {
     const int bin = blockIdx.x * blockDim.x + threadIdx.x;
     if (bin >= a.n) return;
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     const float al = a.ema_alpha;
+#pragma unroll 8
     for (int f = 0; f < a.n_frames; f++) {
-        size_t row;
-        if (a.ring_rows > 0) {
-            int rr = (a.ring_base - f) % a.ring_rows;
-            row = (size_t)(rr < 0 ? rr + a.ring_rows : rr) * a.n;
-        } else {
-            row = (size_t)((long long)f * a.row_stride);
-        }
-        const float x = a.rows[row + bin];
+        const float x = state_row(a, f)[bin];
         pk = fmaxf(pk, x);
         em = (em > -INFINITY) ? em + al * (x - em) : x;
+    }
+    if (a.peaks) a.peaks[bin] = pk;
+    if (a.ema) a.ema[bin] = em;
+}
+
+// Chunked form of the same recursions for large batches: blockIdx.y = chunk of
+// chunk_len frames.  Per (chunk, bin) it stores
+//   x: max over the chunk,
+//   y: (1-alpha)^L, or -1 if some frame of the chunk is -inf (the EMA restarts there),
+//   z: b with  em_out = y * em_in + b  for a finite em_in and no restart,
+//   w: the chunk's EMA started from -inf (= em_out whenever em_in is -inf or the
+//      chunk restarts: after a -inf frame both runs are identical).
+__global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
+    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+    const int c = blockIdx.y;
+    if (bin >= a.n) return;
+    const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
+    const float al = a.ema_alpha, keep = 1.0f - al;
+    float pk = -INFINITY, emi = -INFINITY, am = 1.0f, b = 0.0f;
+    bool restart = false;
+#pragma unroll 8
+    for (int f = f0; f < f1; f++) {
+        const float x = state_row(a, f)[bin];
+        pk = fmaxf(pk, x);
+        emi = (emi > -INFINITY) ? emi + al * (x - emi) : x;
+        restart |= x == -INFINITY;
+        am *= keep;
+        b = b + al * (x - b);
+    }
+    a.part[(size_t)c * a.n + bin] = make_float4(pk, restart ? -1.0f : am, b, emi);
+}
+
+__global__ void state_combine_kernel(StateLaunch a, int chunks) {
+    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bin >= a.n) return;
+    float pk = a.peaks ? a.peaks[bin] : 0.f;
+    float em = a.ema ? a.ema[bin] : 0.f;
+    for (int c = 0; c < chunks; c++) {
+        const float4 p = a.part[(size_t)c * a.n + bin];
+        pk = fmaxf(pk, p.x);
+        em = (em == -INFINITY || p.y < 0.0f) ? p.w : fmaf(p.y, em, p.z);
     }
     if (a.peaks) a.peaks[bin] = pk;
     if (a.ema) a.ema[bin] = em;
@@ -414,7 +460,16 @@ __global__ void state_kernel(StateLaunch a) {
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
     const int tpb = 256;
-    hipLaunchKernelGGL(state_kernel, dim3((a.n + tpb - 1) / tpb), dim3(tpb), 0, a.stream, a);
+    const int bx = (a.n + tpb - 1) / tpb;
+    int chunks = a.part ? std::min(a.max_chunks, (a.n_frames + 7) / 8) : 1;
+    if (chunks > 1) {
+        const int len = (a.n_frames + chunks - 1) / chunks;
+        chunks = (a.n_frames + len - 1) / len;
+        hipLaunchKernelGGL(state_partial_kernel, dim3(bx, chunks), dim3(tpb), 0, a.stream, a, len);
+        hipLaunchKernelGGL(state_combine_kernel, dim3(bx), dim3(tpb), 0, a.stream, a, chunks);
+    } else {
+        hipLaunchKernelGGL(state_kernel, dim3(bx), dim3(tpb), 0, a.stream, a);
+    }
     return hipGetLastError();
 }
 

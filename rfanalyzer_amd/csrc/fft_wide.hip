@@ -166,6 +166,103 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
     for (int b = 0; b < W::NB; b++) dft<16>(&v[b * 16]);
 }
 
+// x * W_16^q added to acc, with the rotation / sqrt(1/2) forms folded in.
+template <int Q>
+__device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
+    constexpr int q = Q & 15;
+    if constexpr ((q & 3) == 0) return padd<0, q / 4>(acc, x);
+    else if constexpr ((q & 3) == 2) return from_v(__builtin_elementwise_fma(to_v(padd<(q - 2) / 4, (q + 2) / 4>(x, x)), (f2v){kR2, kR2}, to_v(acc)));
+    else return cadd(acc, w16<q>(x));
+}
+
+// Decimation-in-frequency pre-stage for N = RS * M, residue R (compile-time):
+//   y_R[m] = W_N^{m R} * sum_j x[m + jM] w[m + jM] W_RS^{j R},   m = tid + TPF b + (M/32) t
+// W_N^{m R} = pre_a[R][tid + TPF b] * pre_b[R][t] (exact tables).  The RS raw
+// samples of a point come from RS separate quarter-frames; the RS window values
+// are adjacent in the interleaved window (one 8/16-byte load).  Loads run one
+// chunk ahead of the arithmetic (software pipeline), so a wave keeps two
+// chunks of L2 requests in flight instead of waiting a full round trip per chunk.
+template <int LOGM, int PT, int RS, int FMT, int R>
+__device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
+                                         int tid, int planar_im) {
+    using G = WGeo<LOGM, PT>;
+    constexpr int M = G::M;
+    constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));  // bytes per sample (per plane)
+    // points per chunk: two chunks of raw samples + window values in flight must
+    // fit beside the PT points in the register budget (64 VGPRs at PT = 32)
+    constexpr int C = (PT == 64 ? 16 : 8) / RS > 0 ? (PT == 64 ? 16 : 8) / RS : 1;
+    constexpr int NCH = PT / C;
+    const rsrc_t w_rs = make_rsrc(window_il, M * RS * 4);
+    const rsrc_t pa_rs = make_rsrc(wide_tw + G::TW_LDS, RS * (M / 32) * 8);
+    const float2 *pre_b = wide_tw + G::TW_LDS + RS * (M / 32) + R * 32;
+    float2 pa[PT / 32];
+    if constexpr (R != 0) {
+#pragma unroll
+        for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, R * (M / 32) * 8);
+    }
+    typename Raw<FMT>::T raw[2][C][RS];
+    float win[2][C][RS];
+    // c is a template parameter throughout: every register array index below is a
+    // compile-time constant (a runtime index would move the arrays to scratch)
+    auto issue = [&]<int c>() {
+        constexpr int s = c & 1;
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+            const int idx = c * C + q, b = idx >> 5, t = idx & 31;
+            const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
+#pragma unroll
+            for (int j = 0; j < RS; j++) raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
+            if constexpr (RS == 2) {
+                const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
+                win[s][q][0] = w.x;
+                win[s][q][1] = w.y;
+            } else {
+#pragma unroll
+                for (int j4 = 0; j4 < RS; j4 += 4) {
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    const f4v w = __builtin_bit_cast(
+                        f4v, __builtin_amdgcn_raw_buffer_load_b128(w_rs, tid * RS * 4, (mo * RS + j4) * 4, 0));
+                    win[s][q][j4] = w.x;
+                    win[s][q][j4 + 1] = w.y;
+                    win[s][q][j4 + 2] = w.z;
+                    win[s][q][j4 + 3] = w.w;
+                }
+            }
+        }
+    };
+    auto compute = [&]<int c>() {
+        constexpr int s = c & 1;
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+            const int idx = c * C + q, b = idx >> 5, t = idx & 31;
+            float2 acc;
+            [&]<int... Js>(std::integer_sequence<int, Js...>) {
+                (
+                    [&] {
+                        const float2 x = convert_raw<FMT>(raw[s][q][Js]);
+                        const float2 xw = from_v(to_v(x) * win[s][q][Js]);  // NativeDsp.kt:55-58 (fp32 multiply)
+                        if constexpr (Js == 0) acc = xw;
+                        else acc = add_w16<(Js * R * (16 / RS)) & 15>(acc, xw);  // W_RS^{j R} = W_16^{j R 16/RS}
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, RS>{});
+            if constexpr (R == 0) v[idx] = acc;
+            else v[idx] = cmul(acc, cmul(pa[b], pre_b[t]));
+        }
+    };
+    issue.template operator()<0>();
+    [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+        (
+            [&] {
+                if constexpr (Cs + 1 < NCH) issue.template operator()<Cs + 1>();
+                __builtin_amdgcn_sched_barrier(0);
+                compute.template operator()<Cs>();
+                __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, NCH>{});
+}
+
 // DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
 // 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
 template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0>
@@ -238,39 +335,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 v[idx] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
             }
         } else {
-            // y_r[m] = W_N^{m r} sum_j x[m + jM] w[m + jM] W_RS^{j r};  m = m' + (M/32) t, m' = tid + TPF b
-            // W_N^{m r} = pre_a[r][m'] * pre_b[r][t]
-            const rsrc_t w_rs = make_rsrc(a.window_il, n * 4);
-            const rsrc_t pa_rs = make_rsrc(a.wide_tw + G::TW_LDS, RS * (M / 32) * 8);
-            const float2 *pre_b = a.wide_tw + G::TW_LDS + RS * (M / 32) + r * 32;
-            float2 wr[RS];  // W_RS^{j r}: wave-uniform
-    #pragma unroll
-            for (int j = 0; j < RS; j++) wr[j] = kW8[((j * r) * (8 / RS)) & 7];
-            float2 pa[PT / 32];
-    #pragma unroll
-            for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, r * (M / 32) * 8);
-    #pragma unroll
-            for (int c = 0; c < PT / 4; c++) {
-    #pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const int idx = c * 4 + q, b = idx >> 5, t = idx & 31;
-                    const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
-                    float wj[RS];
-    #pragma unroll
-                    for (int j = 0; j < RS; j++) wj[j] = buf_load_f32(w_rs, tid * RS * 4, (mo * RS + j) * 4);
-                    float2 acc = make_float2(0.f, 0.f);
-    #pragma unroll
-                    for (int j = 0; j < RS; j++) {
-                        const float2 x = convert_raw<FMT>(
-                            buf_load_raw<FMT>(in_rs, tid * (FMT == 4 ? 4 : BPS), (mo + j * M) * (FMT == 4 ? 4 : BPS),
-                                              planar_im));
-                        const float2 xw = make_float2(x.x * wj[j], x.y * wj[j]);
-                        acc = (j == 0) ? xw : cadd(acc, cmul(xw, wr[j]));
-                    }
-                    v[idx] = (r == 0) ? acc : cmul(acc, cmul(pa[b], pre_b[t]));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
+            // residue r is wave-uniform: instantiate the pre-stage per r so the
+            // W_RS^{j r} factors are compile-time rotations
+            const int planar = planar_im;
+            [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs>(v, a.window_il, a.wide_tw, in_rs, tid, planar) : void()), ...);
+            }(std::make_integer_sequence<int, RS>{});
         }
 
         // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
@@ -417,25 +487,15 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
     if (a.diag) {  // ablations: 16K, s8 only
         if (a.logn != 14 || a.fmt != 0 || co) return hipErrorInvalidValue;
         switch (a.diag) {
-        case 1: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 1>(a) : launch_wide_one<14, 32, 1, 0, false, 1>(a));
-        case 2: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 2>(a) : launch_wide_one<14, 32, 1, 0, false, 2>(a));
-        case 3: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 3>(a) : launch_wide_one<14, 32, 1, 0, false, 3>(a));
-        case 4: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 4>(a) : launch_wide_one<14, 32, 1, 0, false, 4>(a));
-        case 8: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 8>(a) : launch_wide_one<14, 32, 1, 0, false, 8>(a));
-        case 12: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 12>(a) : launch_wide_one<14, 32, 1, 0, false, 12>(a));
-        case 16: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 16>(a) : launch_wide_one<14, 32, 1, 0, false, 16>(a));
-        case 19: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 19>(a) : launch_wide_one<14, 32, 1, 0, false, 19>(a));
-        case 31: return (a.wide_pt == 64 ? launch_wide_one<14, 64, 1, 0, false, 31>(a) : launch_wide_one<14, 32, 1, 0, false, 31>(a));
-        default: return hipErrorInvalidValue;
-        }
-    }
-    if (a.wide_pt == 64) {
-        switch (a.logn) {
-        case 13: return co ? wide_by_fmt<13, 64, 1, true>(a) : wide_by_fmt<13, 64, 1, false>(a);
-        case 14: return co ? wide_by_fmt<14, 64, 1, true>(a) : wide_by_fmt<14, 64, 1, false>(a);
-        case 15: return co ? wide_by_fmt<14, 64, 2, true>(a) : wide_by_fmt<14, 64, 2, false>(a);
-        case 16: return co ? wide_by_fmt<14, 64, 4, true>(a) : wide_by_fmt<14, 64, 4, false>(a);
-        case 17: return co ? wide_by_fmt<14, 64, 8, true>(a) : wide_by_fmt<14, 64, 8, false>(a);
+        case 1: return launch_wide_one<14, 32, 1, 0, false, 1>(a);
+        case 2: return launch_wide_one<14, 32, 1, 0, false, 2>(a);
+        case 3: return launch_wide_one<14, 32, 1, 0, false, 3>(a);
+        case 4: return launch_wide_one<14, 32, 1, 0, false, 4>(a);
+        case 8: return launch_wide_one<14, 32, 1, 0, false, 8>(a);
+        case 12: return launch_wide_one<14, 32, 1, 0, false, 12>(a);
+        case 16: return launch_wide_one<14, 32, 1, 0, false, 16>(a);
+        case 19: return launch_wide_one<14, 32, 1, 0, false, 19>(a);
+        case 31: return launch_wide_one<14, 32, 1, 0, false, 31>(a);
         default: return hipErrorInvalidValue;
         }
     }

@@ -179,6 +179,10 @@ class SpectrumEngine:
     def set_profiling(self, on: bool) -> None:
         self._check(_lib.lib().rfa_set_profiling(self._h, 1 if on else 0), "rfa_set_profiling")
 
+    def main_kernel_name(self) -> str:
+        """HIP kernel that rfa_process launches for this configuration (rocprofv3 name)."""
+        return _lib.lib().rfa_main_kernel_name(self._h).decode()
+
     def kernel_time(self):
         ms, n = ctypes.c_double(), ctypes.c_int64()
         self._check(_lib.lib().rfa_get_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)),

@@ -104,3 +104,27 @@ def test_ema_matches_sequential_extension(rfa):
         e.process(data[2 * n * 20:], b - 20, rows=False)
         got = e.ema()
     assert gu.db_diff(got, processor.ema_batch(ref_rows, 0.2)) <= gu.DB_TOL
+
+
+@pytest.mark.parametrize("batches", [(100,), (13, 87), (1, 2, 97)])
+def test_chunked_state_with_silent_frames(rfa, batches):
+    """Large batches take the chunked peak/EMA update; all-zero frames give
+    -inf rows, which restart the EMA (extension semantics, oracle/processor.py)."""
+    n, total = 2048, sum(batches)
+    raw = np.random.default_rng(11).integers(-128, 128, size=(total, 2 * n), dtype=np.int8)
+    raw[[0, 30, 31, 32, 77, total - 1]] = 0
+    data = raw.tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, total, None, oracle.WIN_BLACKMAN)
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.3, peak_hold=True, ring_rows=0) as e:
+        f = 0
+        for b in batches:
+            e.process(data[f * 2 * n:(f + b) * 2 * n], b, rows=False)
+            f += b
+        ema, peaks = e.ema(), e.peaks()
+    exp = processor.ema_batch(ref_rows, 0.3)
+    assert np.all(np.isneginf(exp)) and np.all(np.isneginf(ema))  # the last frame is silent
+    ema_before = processor.ema_batch(ref_rows[:-1], 0.3)
+    assert gu.db_diff(peaks, ref_rows.max(0)) <= gu.DB_TOL
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.3, ring_rows=0) as e:
+        e.process(data[: (total - 1) * 2 * n], total - 1, rows=False)
+        assert gu.db_diff(e.ema(), ema_before) <= gu.DB_TOL
