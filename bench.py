@@ -74,6 +74,18 @@ def make_pool(torch, n, frames, fmt, pool_mib, seed, device):
     return pool
 
 
+def max_over_ranks(value: float, world: int, device) -> float:
+    """Slowest rank's time: the timed region ends when the last GPU finishes."""
+    if world <= 1:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def cpu_baseline(args, n, seconds):
     """Reference loop (pffft + restated JVM loops, oracle/_ref) on 1 host core, bounded time."""
     import numpy as np
@@ -165,10 +177,7 @@ def main():
     elapsed = time.perf_counter() - t0
     ms1, l1 = eng.kernel_time()
     eng.set_profiling(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, world, device)
 
     samples = world * args.steps * frames * n
     msps = samples / elapsed / 1e6

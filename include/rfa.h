@@ -160,6 +160,11 @@ RFA_API int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n
  * the handle stream and the summed device time is reported. */
 RFA_API int rfa_set_profiling(rfa_handle *h, int enable);
 RFA_API int rfa_get_kernel_time(rfa_handle *h, double *total_ms, int64_t *launches);
+/* Host-only helper (no device work): the waterfall shift in bins applied by
+ * rfa_set_tuning for a retune by frequency_diff = last_frequency - frequency,
+ * ((lastF - f) * (N / sampleRate.toFloat())).toInt() in fp32 with Kotlin's
+ * truncating, saturating Float.toInt() (FftProcessor.kt:143,173,199). */
+RFA_API int64_t rfa_retune_offset(int64_t frequency_diff, int n, int64_t sample_rate);
 /* Name of the HIP kernel rfa_process launches for this handle's configuration
  * ("fft_wide_kernel" or "fft_rows_kernel"), as rocprofv3 reports it. */
 RFA_API const char *rfa_main_kernel_name(const rfa_handle *h);

@@ -533,6 +533,17 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
     return RFA_OK;
 }
 
+int64_t rfa_retune_offset(int64_t frequency_diff, int n, int64_t sample_rate) {
+    if (sample_rate <= 0) return 0;
+    // FftProcessor.kt:143,199: (fdiff * (N / sampleRate.toFloat())).toInt(), float arithmetic
+    const float samples_per_hz = (float)n / (float)sample_rate;
+    const float prod = (float)frequency_diff * samples_per_hz;
+    if (std::isnan(prod)) return 0;
+    if (prod >= 2147483647.0f) return 2147483647LL;
+    if (prod <= -2147483648.0f) return -2147483648LL;
+    return (int64_t)prod;  // truncation toward zero
+}
+
 int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
     if (!h || sample_rate <= 0) return RFA_ERR_INVALID;
     int rc = set_device(h);
@@ -551,14 +562,7 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
     h->last_sample_rate = sample_rate;
     if (h->d_ring) {
         if (fdiff != 0) {
-            // FftProcessor.kt:143,199: (fdiff * (N / sampleRate.toFloat())).toInt(), float arithmetic
-            const float samples_per_hz = (float)h->n / (float)sample_rate;
-            const float prod = (float)fdiff * samples_per_hz;
-            long long off;
-            if (std::isnan(prod)) off = 0;
-            else if (prod >= 2147483647.0f) off = 2147483647LL;
-            else if (prod <= -2147483648.0f) off = -2147483648LL;
-            else off = (long long)prod;  // truncation toward zero
+            const long long off = rfa_retune_offset(fdiff, h->n, sample_rate);
             if ((off < 0 && -off < h->n) || (off >= 0 && off < h->n)) {
                 HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, (int)off, kRingFill,
                                                  h->stream));

@@ -26,38 +26,40 @@ def frame_range(n_frames: int, rank: int, world: int) -> tuple[int, int]:
 
 
 def ema_partial(rows: np.ndarray, alpha: float):
-    """Segment summary for the EMA: (partial, first_row, decay, restarted) with
-    partial = sum_k alpha (1-alpha)^(m-1-k) x_k and decay = (1-alpha)^m.
-    Bins that see a -inf inside the segment restart there (the state becomes
-    -inf and the next frame re-seeds it): for them `restarted` is set and
-    `partial` already holds the exact end state."""
-    a = np.float64(alpha)
-    m = rows.shape[0]
-    partial = np.zeros(rows.shape[1], np.float64)
-    restarted = np.zeros(rows.shape[1], bool)
-    fresh = np.full(rows.shape[1], np.nan)
-    for k in range(m):
-        x = rows[k].astype(np.float64)
-        neg = np.isneginf(x)
-        # bins restarted earlier follow the sequential rule on `fresh`
-        fresh = np.where(restarted, np.where(np.isneginf(fresh) | np.isnan(fresh), x, fresh + a * (x - fresh)), fresh)
-        newly = neg & ~restarted
-        fresh = np.where(newly, -np.inf, fresh)
-        restarted |= neg
-        partial = (1 - a) * partial + a * x
-    partial = np.where(restarted, fresh, partial)
-    return partial, rows[0].astype(np.float64), float((1 - a) ** m), restarted
+    """Segment summary of the EMA over `rows` (m frames), the same form the
+    chunked device update uses (state_partial_kernel, fft_kernels.hip):
+
+    ``(decay, b, fresh)`` with ``em_out = decay * em_in + b`` for a finite
+    ``em_in`` when no frame of the segment is -inf for that bin, and
+    ``em_out = fresh`` (the segment's EMA started from -inf) when ``em_in`` is
+    -inf or the segment restarts (after a -inf frame both runs coincide).
+    ``decay`` is -1 for bins that restart."""
+    al = np.float32(alpha)
+    keep = np.float32(1) - al
+    n = rows.shape[1]
+    am = np.ones(n, np.float32)
+    b = np.zeros(n, np.float32)
+    fresh = np.full(n, -np.inf, np.float32)
+    restart = np.zeros(n, bool)
+    with np.errstate(invalid="ignore"):
+        for x in np.asarray(rows, np.float32):
+            fresh = np.where(fresh > -np.inf, fresh + al * (x - fresh), x).astype(np.float32)
+            restart |= np.isneginf(x)
+            am = (am * keep).astype(np.float32)
+            b = (b + al * (x - b)).astype(np.float32)
+    return np.where(restart, np.float32(-1), am), b, fresh
 
 
 def ema_combine(state: np.ndarray | None, segments) -> np.ndarray:
-    """Fold segment summaries (from `ema_partial`) in order; `state` None/-inf = uninitialised."""
-    s = None if state is None else np.asarray(state, np.float64).copy()
-    for partial, first, decay, restarted in segments:
-        if s is None:
-            s = np.full(partial.shape, -np.inf)
-        init = np.where(s > -np.inf, s, first)
-        s = np.where(restarted, partial, decay * init + partial)
-    return s.astype(np.float32)
+    """Fold segment summaries (from `ema_partial`) in frame order; `state`
+    None or -inf = uninitialised (the first frame seeds the average)."""
+    em = None if state is None else np.asarray(state, np.float32).copy()
+    for decay, b, fresh in segments:
+        if em is None:
+            em = np.full(b.shape, -np.inf, np.float32)
+        with np.errstate(invalid="ignore"):
+            em = np.where((em == -np.inf) | (decay < 0), fresh, decay * em + b).astype(np.float32)
+    return em
 
 
 def peak_combine(parts) -> np.ndarray:
