@@ -86,7 +86,7 @@ def max_over_ranks(value: float, world: int, device) -> float:
     return float(t.item())
 
 
-def cpu_baseline(args, n, seconds):
+def cpu_baseline(args, n, seconds, threads=1):
     """Reference loop (pffft + restated JVM loops, oracle/_ref) on 1 host core, bounded time."""
     import numpy as np
 
@@ -105,30 +105,70 @@ def cpu_baseline(args, n, seconds):
         data = iq.astype(np.float32)
     w = oracle.window(n, oracle.WIN_BLACKMAN)
     ring_rows = 500
-    done, t0 = 0, time.perf_counter()
-    if oracle.ref_available():
+    fp = ctypes.POINTER(ctypes.c_float)
+
+    def run_ref(budget):
+        """One thread = one reference FftProcessor loop (own ring + peaks)."""
         lib = oracle.ref()
         ring = np.full((ring_rows, n), -9999, np.float32)
         peaks = np.full(n, -999999, np.float32)
-        fp = ctypes.POINTER(ctypes.c_float)
-        while time.perf_counter() - t0 < seconds:
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
             rc = lib.ref_loop(data.ctypes.data, fmt, n, frames, n * (2 if fmt == 0 else 8), w.ctypes.data_as(fp),
                               ring.ctypes.data_as(fp), ring_rows, peaks.ctypes.data_as(fp))
             assert rc == 0
             done += frames
+        return done, time.perf_counter() - t0
+
+    if oracle.ref_available():
+        done, el = run_ref(seconds)
         kind = "reference"
         what = ("reference pffft.c (oracle/_ref, -O3 -ffast-math) + restated FftProcessor loop: LUT convert, "
                 "Blackman, FFT, log-mag+shift, ring copy, peak-hold")
     else:
+        done, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < seconds:
             oracle.spectrum_rows(data, fmt, n, frames, None, oracle.WIN_BLACKMAN)
             done += frames
+        el = time.perf_counter() - t0
         kind = "port"
         what = "oracle C restatement (float64 FFT) -- reference pffft build absent"
-    el = time.perf_counter() - t0
-    return {"value": round(done * n / el / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": kind,
-            "sample": f"{frames} x {n}-pt {'s8' if fmt == 0 else 'f32'} frames looped for {el:.1f} s; {what}",
-            "lines_per_s": round(done / el, 2)}
+    out = {"value": round(done * n / el / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": kind,
+           "sample": f"{frames} x {n}-pt {'s8' if fmt == 0 else 'f32'} frames looped for {el:.1f} s; {what}",
+           "lines_per_s": round(done / el, 2)}
+    if kind == "reference" and threads > 1:
+        # frame-parallel on the host's cores (SURVEY.md §8(d)): one independent loop per thread;
+        # ctypes releases the GIL for the duration of each ref_loop call
+        import threading
+
+        res = [None] * threads
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, run_ref(seconds / 2))) for i in range(threads)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        el = max(r[1] for r in res)
+        out["multi_core"] = {"value": round(sum(r[0] for r in res) * n / el / 1e6, 3), "cores": threads,
+                             "sample": f"{threads} threads x the same loop for {el:.1f} s"}
+    return out
+
+
+def copy_ceiling(torch, device, mib=1024, iters=10):
+    """Device stream-copy ceiling in the same run (SURVEY.md §8(d) primary denominator):
+    torch's copy kernel over two 1 GiB buffers, GB/s = 2 x bytes / time."""
+    src = torch.empty(mib * 2 ** 20 // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2 * src.numel() * 4 * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    return round(gbps, 1)
 
 
 def main():
@@ -220,8 +260,11 @@ def main():
                      "kernel": eng.main_kernel_name(), "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if rank == 0 and world == 1:
+        result["roofline"]["copy_GBps"] = copy_ceiling(torch, device)
+        result["roofline"]["frac_of_copy"] = round(achieved / result["roofline"]["copy_GBps"], 4)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds, min(16, os.cpu_count() or 1))
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

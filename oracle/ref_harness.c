@@ -87,12 +87,20 @@ int ref_fft_logmag(const float *in_interleaved, int n, float *mag_out) {
  * Returns 0 on success.  `ring` holds ring_rows*n floats, `peaks` n floats. */
 int ref_loop(const void *frames, int fmt, int n, int n_frames, long frame_stride_bytes, const float *window,
              float *ring, int ring_rows, float *peaks) {
-    if (ensure(n)) return -1;
+    /* a private context per call (one per FftProcessor thread): the multi-core
+     * baseline runs one loop per host thread */
+    ref_ctx c;
+    c.n = n;
+    c.setup = pffft_new_setup(n, PFFFT_COMPLEX);
+    if (!c.setup) return -1;
+    c.scratch = (float *)pffft_aligned_malloc(2 * (size_t)n * sizeof(float));
+    c.in = (float *)pffft_aligned_malloc(2 * (size_t)n * sizeof(float));
+    c.out = (float *)pffft_aligned_malloc(2 * (size_t)n * sizeof(float));
     float lut[256];
     for (int i = 0; i < 256; i++) lut[i] = (float)(i - 128) / 128.0f;
     float *re = (float *)malloc(sizeof(float) * n), *im = (float *)malloc(sizeof(float) * n);
     float *mag = (float *)malloc(sizeof(float) * n);
-    if (!re || !im || !mag) { free(re); free(im); free(mag); return -1; }
+    if (!re || !im || !mag || !c.scratch || !c.in || !c.out) { free(re); free(im); free(mag); return -1; }
     int write_index = 0;
     for (int f = 0; f < n_frames; f++) {
         const uint8_t *p = (const uint8_t *)frames + (size_t)f * frame_stride_bytes;
@@ -103,14 +111,18 @@ int ref_loop(const void *frames, int fmt, int n, int n_frames, long frame_stride
             const float *s = (const float *)p;
             for (int i = 0; i < n; i++) { re[i] = s[2 * i]; im[i] = s[2 * i + 1]; }
         }
-        for (int i = 0; i < n; i++) { g_ctx.in[2 * i] = re[i] * window[i]; g_ctx.in[2 * i + 1] = im[i] * window[i]; }
-        pffft_transform_ordered(g_ctx.setup, g_ctx.in, g_ctx.out, g_ctx.scratch, PFFFT_FORWARD);
-        logmag_shift(g_ctx.out, n, mag);
+        for (int i = 0; i < n; i++) { c.in[2 * i] = re[i] * window[i]; c.in[2 * i + 1] = im[i] * window[i]; }
+        pffft_transform_ordered(c.setup, c.in, c.out, c.scratch, PFFFT_FORWARD);
+        logmag_shift(c.out, n, mag);
         float *row = ring + (size_t)write_index * n;
         memcpy(row, mag, sizeof(float) * n);
         write_index = write_index == 0 ? ring_rows - 1 : write_index - 1;
         for (int i = 0; i < n; i++) peaks[i] = fmaxf(peaks[i], row[i]);
     }
     free(re); free(im); free(mag);
+    pffft_destroy_setup(c.setup);
+    pffft_aligned_free(c.scratch);
+    pffft_aligned_free(c.in);
+    pffft_aligned_free(c.out);
     return 0;
 }
