@@ -37,6 +37,7 @@ struct rfa_handle {
     long long stagger_ns = 0;         // RFA_STAGGER_NS
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
+    int wide_big = 15;                // RFA_WIDE_LOGM: 15 (32 K workgroups) or 14 for N > 16 K
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
@@ -192,6 +193,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.diag = h->diag;
     a.persist = h->persist;
     a.stagger_ns = h->stagger_ns;
+    a.wide_big = h->wide_big;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
     if (a.window == h->d_window) a.window_il = h->d_window_il;
@@ -310,8 +312,10 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMalloc(tabs[i], n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(*tabs[i], src[i], n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
     }
-    if (n > 16384) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
-        const int m_sub = 16384, rs = n / m_sub;
+    if (const char *d = std::getenv("RFA_WIDE_LOGM")) h->wide_big = std::atoi(d) == 14 ? 14 : 15;
+    const int m_sub = 1 << rfa::wide_logm(logn, h->wide_big);
+    if (n > m_sub) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
+        const int rs = n / m_sub;
         std::vector<float> il(n);
         for (int m = 0; m < m_sub; m++)
             for (int j = 0; j < rs; j++) il[(size_t)m * rs + j] = w[(size_t)m + (size_t)j * m_sub];
@@ -320,7 +324,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
             return bail(RFA_ERR_HIP);
     }
     if (rfa::wide_supported(logn)) {
-        std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT);
+        std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn, h->wide_big));
         if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_wide_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);

@@ -38,6 +38,7 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    int wide_big = 15;        // wide_logm() for N > 16 K (RFA_WIDE_LOGM)
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
     int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
@@ -51,7 +52,10 @@ hipError_t launch_fft(const FftLaunch &a);
 // The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
 bool wide_supported(int logn);
 constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
-std::vector<float2> wide_twiddles(int logn, int pt);
+// sub-FFT size of the wide kernel: N itself up to 16 K, else 2^big (15: one
+// 32 K-point workgroup per CU; 14: 16 K, two per CU) with N / 2^big residues
+inline int wide_logm(int logn, int big) { return logn <= 14 ? logn : big; }
+std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at

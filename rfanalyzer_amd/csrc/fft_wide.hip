@@ -35,13 +35,14 @@ struct WGeo {
     static constexpr int SLOTS = THREADS / TPF;  // sub-FFTs per workgroup
     static constexpr int HALF = M / 2;           // exchange buffer (float2) per slot ...
     static constexpr int HALFP = HALF + HALF / 32;  // ... with one float2 of padding per 32
-    static constexpr int R1 = LOGM == 14 ? 32 : 16;  // radix of pass 1 (pass 0: 32, pass 2: 16)
+    static constexpr int R1 = LOGM >= 14 ? 32 : 16;  // radix of pass 1 (pass 0: 32)
+    static constexpr int R2 = M / (32 * R1);          // radix of pass 2: 16 (8 K, 16 K) or 32 (32 K)
     // LDS twiddle tables (float2, t = 1..R-1 only).  Odd row strides (R-1)
     // spread the rows read by one lane group over distinct banks.
     static constexpr int P1_ROW = R1 - 1;        // pass 1: [k = tid & 31][t]
     static constexpr int TW_P1 = 32 * P1_ROW;
     static constexpr int LO = TPF > 256 ? 32 : 16;  // pass 2: tid = hi*LO + lo
-    static constexpr int P2_ROW = 15;
+    static constexpr int P2_ROW = R2 - 1;
     static constexpr int TW_P2A = (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
     static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
     static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
@@ -51,7 +52,7 @@ struct WGeo {
 template <int Q, int LOGM, int PT>
 struct WPass {
     using G = WGeo<LOGM, PT>;
-    static constexpr int R = Q == 0 ? 32 : (Q == 1 ? G::R1 : 16);
+    static constexpr int R = Q == 0 ? 32 : (Q == 1 ? G::R1 : G::R2);
     static constexpr int P = Q == 0 ? 1 : (Q == 1 ? 32 : 32 * G::R1);  // product of earlier radices
     static constexpr int NB = PT / R;                                 // butterflies per thread
     static constexpr int STRIDE = G::M / R;                           // input stride of a butterfly
@@ -132,38 +133,38 @@ __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *tw
     for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
 }
 
-// Pass 2 (last): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_PT^{t b}
+// Pass 2 (last, radix R2): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_PT^{t b}
 // (M / TPF = PT); W_M^{t tid} = A[tid/LO][t] * B[tid%LO][t] from two exact
 // tables, the b-dependent factor is a compile-time constant.
-template <int PT, int T, int B>
+template <int PT, int R2, int T, int B>
 __device__ __forceinline__ void p2_const(float2 (&v)[PT]) {
-    v[B * 16 + T] = w64<T * B * (64 / PT)>(v[B * 16 + T]);
+    v[B * R2 + T] = w64<T * B * (64 / PT)>(v[B * R2 + T]);
 }
-template <int PT, int T, int... Bs>
+template <int PT, int R2, int T, int... Bs>
 __device__ __forceinline__ void p2_const_t(float2 (&v)[PT], std::integer_sequence<int, Bs...>) {
-    (p2_const<PT, T, Bs + 1>(v), ...);
+    (p2_const<PT, R2, T, Bs + 1>(v), ...);
 }
-template <int PT, int... Ts>
+template <int PT, int R2, int... Ts>
 __device__ __forceinline__ void p2_const_all(float2 (&v)[PT], std::integer_sequence<int, Ts...>) {
-    (p2_const_t<PT, Ts>(v, std::make_integer_sequence<int, PT / 16 - 1>{}), ...);
+    (p2_const_t<PT, R2, Ts>(v, std::make_integer_sequence<int, PT / R2 - 1>{}), ...);
 }
 
 template <int LOGM, int PT>
 __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *twp2) {
     using G = WGeo<LOGM, PT>;
     using W = WPass<2, LOGM, PT>;
-    static_assert(W::R == 16, "pass 2 layout");
+    constexpr int R2 = G::R2;
     const float2 *ra = twp2 + (tid / G::LO) * G::P2_ROW - 1;
     const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
 #pragma unroll
-    for (int t = 1; t < 16; t++) {
+    for (int t = 1; t < R2; t++) {
         const float2 w = cmul(ra[t], rb[t]);
 #pragma unroll
-        for (int b = 0; b < W::NB; b++) v[b * 16 + t] = cmul(v[b * 16 + t], w);
+        for (int b = 0; b < W::NB; b++) v[b * R2 + t] = cmul(v[b * R2 + t], w);
     }
-    p2_const_all<PT>(v, std::make_integer_sequence<int, 16>{});
+    if constexpr (W::NB > 1) p2_const_all<PT, R2>(v, std::make_integer_sequence<int, R2>{});
 #pragma unroll
-    for (int b = 0; b < W::NB; b++) dft<16>(&v[b * 16]);
+    for (int b = 0; b < W::NB; b++) dft<R2>(&v[b * R2]);
 }
 
 // x * W_16^q added to acc, with the rotation / sqrt(1/2) forms folded in.
@@ -361,10 +362,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (COMPLEX_OUT) {
             const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * n, n * 8);
     #pragma unroll
-            for (int b = 0; b < PT / 16; b++)
+            for (int b = 0; b < PT / G::R2; b++)
     #pragma unroll
-                for (int t = 0; t < 16; t++)
-                    buf_store_f32x2(v[b * 16 + t], o_rs, (RS * tid + r) * 8, RS * (G::TPF * b + t * (M / 16)) * 8);
+                for (int t = 0; t < G::R2; t++)
+                    buf_store_f32x2(v[b * G::R2 + t], o_rs, (RS * tid + r) * 8,
+                                    RS * (G::TPF * b + t * (M / G::R2)) * 8);
         } else {
             constexpr float db_off = -kDbPerLog2 * (float)(2 * (LOGM + (RS == 1 ? 0 : RS == 2 ? 1 : RS == 4 ? 2 : 3)));
             const bool to_ring = a.ring && frame >= a.ring_first;
@@ -379,13 +381,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // one uniform branch per item, not per store
             auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
     #pragma unroll
-                for (int b = 0; b < PT / 16; b++) {
+                for (int b = 0; b < PT / G::R2; b++) {
     #pragma unroll
-                    for (int t = 0; t < 16; t++) {
-                        const float2 x = v[b * 16 + t];
+                    for (int t = 0; t < G::R2; t++) {
+                        const float2 x = v[b * G::R2 + t];
                         const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
                         // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
-                        const int so = ((RS * (G::TPF * b + t * (M / 16)) + n / 2) & (n - 1)) * 4;
+                        const int so = ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
                         if constexpr (DIAG & 2) {
                             asm volatile("" ::"v"(db));
                         } else {
@@ -459,9 +461,9 @@ bool wide_supported(int logn) { return logn >= 13 && logn <= 17; }
 
 // Twiddle blob for the wide kernel (layout must match WGeo): pass-1 [32][R1-1],
 // pass-2 A [TPF/LO][15], B [LO][15], pre-stage pre_a [RS][M/32], pre_b [RS][32].
-std::vector<float2> wide_twiddles(int logn, int pt) {
-    const int lm = logn == 13 ? 13 : 14, m = 1 << lm, n = 1 << logn, rs = n / m;
-    const int r1 = lm == 14 ? 32 : 16, tpf = m / pt, lo = tpf > 256 ? 32 : 16;
+std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
+    const int m = 1 << lm, n = 1 << logn, rs = n / m;
+    const int r1 = lm >= 14 ? 32 : 16, r2 = m / (32 * r1), tpf = m / pt, lo = tpf > 256 ? 32 : 16;
     auto w = [](double num, double den) {  // exp(-2 pi i num/den), correctly rounded from double
         const double a = -2.0 * M_PI * num / den;
         return make_float2((float)std::cos(a), (float)std::sin(a));
@@ -470,9 +472,9 @@ std::vector<float2> wide_twiddles(int logn, int pt) {
     for (int k = 0; k < 32; k++)
         for (int t = 1; t < r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
     for (int hi = 0; hi < tpf / lo; hi++)
-        for (int t = 1; t < 16; t++) blob.push_back(w((double)t * hi * lo, m));
+        for (int t = 1; t < r2; t++) blob.push_back(w((double)t * hi * lo, m));
     for (int l = 0; l < lo; l++)
-        for (int t = 1; t < 16; t++) blob.push_back(w((double)t * l, m));
+        for (int t = 1; t < r2; t++) blob.push_back(w((double)t * l, m));
     if (rs > 1) {
         for (int r = 0; r < rs; r++)
             for (int mp = 0; mp < m / 32; mp++) blob.push_back(w((double)mp * r, n));
@@ -496,6 +498,14 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         case 16: return launch_wide_one<14, 32, 1, 0, false, 16>(a);
         case 19: return launch_wide_one<14, 32, 1, 0, false, 19>(a);
         case 31: return launch_wide_one<14, 32, 1, 0, false, 31>(a);
+        default: return hipErrorInvalidValue;
+        }
+    }
+    if (a.logn >= 15 && a.wide_big == 15) {
+        switch (a.logn) {
+        case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
+        case 16: return co ? wide_by_fmt<15, 32, 2, true>(a) : wide_by_fmt<15, 32, 2, false>(a);
+        case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
         default: return hipErrorInvalidValue;
         }
     }
