@@ -86,15 +86,36 @@ RFA_HD float2 cmul(float2 a_, float2 w_) {
     return make_float2(fmaf(a_.x, w_.x, -a_.y * w_.y), fmaf(a_.x, w_.y, a_.y * w_.x));
 #endif
 }
+// two independent complex multiplies a0*w0, a1*w1 interleaved in one block, so
+// no multiply is immediately followed by its dependent fma (gfx950 inserts an
+// s_nop between a packed write and a dependent packed read)
+RFA_HD void cmul2(float2 &a0_, float2 w0_, float2 &a1_, float2 w1_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    f2v a0 = to_v(a0_), a1 = to_v(a1_);
+    const f2v w0 = to_v(w0_), w1 = to_v(w1_);
+    f2v m0, m1;  // early-clobber: written before the other pair's operands are read
+    asm("v_pk_mul_f32 %0, %2, %4 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %1, %3, %5 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %2, %2, %4, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %3, %3, %5, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=&v"(m0), "=&v"(m1), "+v"(a0), "+v"(a1)
+        : "v"(w0), "v"(w1));
+    a0_ = from_v(a0);
+    a1_ = from_v(a1);
+#else
+    a0_ = cmul(a0_, w0_);
+    a1_ = cmul(a1_, w1_);
+#endif
+}
+
 // complex a * (c, s) for a compile-time constant (held in an SGPR pair)
+// (plain vector code: both constant pairs live in SGPRs, hipcc emits v_pk_mul +
+// v_pk_fma and is free to interleave independent multiplies)
 RFA_HD float2 cmulc(float2 a_, float c, float s) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const f2v a = to_v(a_), w = {c, s};
-    f2v m, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(m) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r) : "v"(a), "s"(w), "v"(m));
-    return from_v(r);
+    const f2v a = to_v(a_);
+    const f2v m = (f2v){a.x, a.x} * (f2v){c, s};
+    return from_v(__builtin_elementwise_fma((f2v){a.y, a.y}, (f2v){-s, c}, m));
 #else
     return make_float2(fmaf(a_.x, c, -a_.y * s), fmaf(a_.x, s, a_.y * c));
 #endif

@@ -124,10 +124,10 @@ __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *tw
     using W = WPass<1, LOGM, PT>;
     const float2 *row = twp1 + (tid & 31) * WGeo<LOGM, PT>::P1_ROW - 1;
 #pragma unroll
-    for (int t = 1; t < W::R; t++) {
-        const float2 w = row[t];
+    for (int b = 0; b < W::NB; b++) {
+        v[b * W::R + 1] = cmul(v[b * W::R + 1], row[1]);
 #pragma unroll
-        for (int b = 0; b < W::NB; b++) v[b * W::R + t] = cmul(v[b * W::R + t], w);
+        for (int t = 2; t < W::R; t += 2) cmul2(v[b * W::R + t], row[t], v[b * W::R + t + 1], row[t + 1]);
     }
 #pragma unroll
     for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
@@ -156,11 +156,17 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
     constexpr int R2 = G::R2;
     const float2 *ra = twp2 + (tid / G::LO) * G::P2_ROW - 1;
     const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
+    {
+        const float2 w1 = cmul(ra[1], rb[1]);
 #pragma unroll
-    for (int t = 1; t < R2; t++) {
-        const float2 w = cmul(ra[t], rb[t]);
+        for (int b = 0; b < W::NB; b++) v[b * R2 + 1] = cmul(v[b * R2 + 1], w1);
+    }
 #pragma unroll
-        for (int b = 0; b < W::NB; b++) v[b * R2 + t] = cmul(v[b * R2 + t], w);
+    for (int t = 2; t < R2; t += 2) {  // twiddle pairs built and applied in place (no table in VGPRs)
+        float2 w0 = ra[t], w1 = ra[t + 1];
+        cmul2(w0, rb[t], w1, rb[t + 1]);
+#pragma unroll
+        for (int b = 0; b < W::NB; b++) cmul2(v[b * R2 + t], w0, v[b * R2 + t + 1], w1);
     }
     if constexpr (W::NB > 1) p2_const_all<PT, R2>(v, std::make_integer_sequence<int, R2>{});
 #pragma unroll
@@ -233,10 +239,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     };
     auto compute = [&]<int c>() {
         constexpr int s = c & 1;
+        float2 accs[C];
 #pragma unroll
         for (int q = 0; q < C; q++) {
-            const int idx = c * C + q, b = idx >> 5, t = idx & 31;
-            float2 acc;
+            float2 &acc = accs[q];
             [&]<int... Js>(std::integer_sequence<int, Js...>) {
                 (
                     [&] {
@@ -247,8 +253,23 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
                     }(),
                     ...);
             }(std::make_integer_sequence<int, RS>{});
-            if constexpr (R == 0) v[idx] = acc;
-            else v[idx] = cmul(acc, cmul(pa[b], pre_b[t]));
+        }
+        // twiddle W_N^{m R} = pre_a * pre_b, then acc * twiddle: independent pairs interleaved
+#pragma unroll
+        for (int q = 0; q < C; q += 2) {
+            const int i0 = c * C + q;
+            if constexpr (R == 0) {
+                v[i0] = accs[q];
+                if (q + 1 < C) v[i0 + 1] = accs[q + 1];
+            } else if (q + 1 < C) {
+                float2 w0 = pa[i0 >> 5], w1 = pa[(i0 + 1) >> 5];
+                cmul2(w0, pre_b[i0 & 31], w1, pre_b[(i0 + 1) & 31]);
+                cmul2(accs[q], w0, accs[q + 1], w1);
+                v[i0] = accs[q];
+                v[i0 + 1] = accs[q + 1];
+            } else {
+                v[i0] = cmul(accs[q], cmul(pa[i0 >> 5], pre_b[i0 & 31]));
+            }
         }
     };
     issue.template operator()<0>();
