@@ -31,7 +31,14 @@ struct rfa_handle {
     float *d_window_none = nullptr;   // all ones (already-windowed f32 seams)
     float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
     float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
-    float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17)
+    float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17, and kernel A for larger N)
+    // N = 2^18..2^20 (decimation in time, fft_large.hip)
+    float *d_dit_window = nullptr;    // scaled window permuted to [S][M]: w[S m + r] at [r][m]
+    float *d_dit_black = nullptr;     // unscaled Blackman, same permutation (NativeDsp.kt seam)
+    float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{r k} = C[r][k >> 7] * D[r][k & 127]
+    float2 *d_dit_y = nullptr;        // scratch [frames][S][M] complex
+    size_t d_dit_y_cap = 0;
+    int dit_frames = 1;               // frames per kernel-A/B pair (scratch <= kDitScratch)
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
@@ -184,6 +191,47 @@ hipEvent_t get_event(rfa_handle *h) {
     return e;
 }
 
+// N = 2^18..2^20: kernel A (wide kernel on the S strided sub-frames, complex out
+// to scratch) + kernel B (radix-S combine, dB rows / ring / complex out), in
+// batches of dit_frames frames so the scratch stays cache resident.
+static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
+    const int n = h->n, s = n >> rfa::kDitLogM;
+    const float *win = a.window == h->d_window         ? h->d_dit_window
+                       : a.window == h->d_window_black ? h->d_dit_black
+                                                       : a.window;  // all-ones table: any layout
+    for (int f0 = 0; f0 < a.n_frames; f0 += h->dit_frames) {
+        const int cnt = std::min(h->dit_frames, a.n_frames - f0);
+        FftLaunch A = a;
+        A.in = a.in + (size_t)f0 * (size_t)a.frame_stride;
+        A.n_frames = cnt;
+        A.dit_ss = s;
+        A.window = win;
+        A.rows = nullptr;
+        A.ring = nullptr;
+        A.complex_out = h->d_dit_y;
+        hipError_t e = rfa::launch_fft_wide(A);
+        if (e != hipSuccess) return e;
+        rfa::DitLaunch B;
+        B.y = h->d_dit_y;
+        B.n_frames = cnt;
+        B.frame0 = f0;
+        B.logn = h->logn;
+        B.logm = rfa::kDitLogM;
+        B.tw_c = h->d_dit_c;
+        B.tw_d = h->d_dit_d;
+        B.rows = a.rows ? a.rows + (size_t)f0 * n : nullptr;
+        B.ring = a.ring;
+        B.ring_rows = a.ring_rows;
+        B.ring_base = a.ring_base;
+        B.ring_first = a.ring_first;
+        B.complex_out = a.complex_out ? a.complex_out + (size_t)f0 * n : nullptr;
+        B.stream = a.stream;
+        e = rfa::launch_dit_combine(B);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 int launch_main(rfa_handle *h, FftLaunch &a) {
     a.stream = h->stream;
     a.logn = h->logn;
@@ -206,7 +254,20 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         e1 = get_event(h);
         hipEventRecord(e0, h->stream);
     }
-    hipError_t e = rfa::launch_fft(a);
+    hipError_t e = hipSuccess;
+    if (h->logn > 17) {
+        const size_t need = (size_t)std::min(h->dit_frames, a.n_frames) * h->n * sizeof(float2);
+        if (need > h->d_dit_y_cap) {
+            hipFree(h->d_dit_y);
+            h->d_dit_y = nullptr;
+            h->d_dit_y_cap = 0;
+            if (hipMalloc(&h->d_dit_y, need) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "large-N scratch");
+            h->d_dit_y_cap = need;
+        }
+        e = launch_large(h, a);
+    } else {
+        e = rfa::launch_fft(a);
+    }
     if (h->profile) {
         hipEventRecord(e1, h->stream);
         h->ev_pending.emplace_back(e0, e1);
@@ -274,7 +335,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     *out = nullptr;
     const int logn = ilog2_exact(cfg->fft_size);
     if (logn < 0 || cfg->fft_size < RFA_MIN_FFT_SIZE || cfg->fft_size > RFA_MAX_FFT_SIZE) return RFA_ERR_UNSUPPORTED;
-    if (logn > rfa::kMaxLogM + rfa::kMaxLogSplit) return RFA_ERR_UNSUPPORTED;  // two-pass large-N path pending
+    if (logn > rfa::kMaxLogN) return RFA_ERR_UNSUPPORTED;
     if (cfg->window < 0 || cfg->window > RFA_WINDOW_NONE) return RFA_ERR_INVALID;
     if (bytes_per_sample(cfg->input_format) == 0) return RFA_ERR_INVALID;
     if (cfg->avg_mode < RFA_AVG_NONE || cfg->avg_mode > RFA_AVG_EMA) return RFA_ERR_INVALID;
@@ -314,7 +375,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     }
     if (const char *d = std::getenv("RFA_WIDE_LOGM")) h->wide_big = std::atoi(d) == 14 ? 14 : 15;
     const int m_sub = 1 << rfa::wide_logm(logn, h->wide_big);
-    if (n > m_sub) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
+    if (n > m_sub && logn <= 17) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
         const int rs = n / m_sub;
         std::vector<float> il(n);
         for (int m = 0; m < m_sub; m++)
@@ -322,6 +383,29 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMalloc(&h->d_window_il, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
+    }
+    if (logn > 17) {  // decimation in time: S strided sub-frames of M = 32768 points
+        const int m = 1 << rfa::kDitLogM, s = n / m;
+        std::vector<float> pw(n), pb(n);
+        for (int r = 0; r < s; r++)
+            for (int i = 0; i < m; i++) {
+                pw[(size_t)r * m + i] = w[(size_t)s * i + r];
+                pb[(size_t)r * m + i] = black[(size_t)s * i + r];
+            }
+        std::vector<float2> c, d, blob = rfa::wide_twiddles(rfa::kDitLogM, rfa::kWidePT, rfa::kDitLogM);
+        rfa::dit_twiddles(logn, c, d);
+        struct { void **dst; const void *src; size_t bytes; } up[] = {
+            {(void **)&h->d_dit_window, pw.data(), pw.size() * sizeof(float)},
+            {(void **)&h->d_dit_black, pb.data(), pb.size() * sizeof(float)},
+            {(void **)&h->d_dit_c, c.data(), c.size() * sizeof(float2)},
+            {(void **)&h->d_dit_d, d.data(), d.size() * sizeof(float2)},
+            {(void **)&h->d_wide_tw, blob.data(), blob.size() * sizeof(float2)}};
+        for (auto &u : up) {
+            if (hipMalloc(u.dst, u.bytes) != hipSuccess) return bail(RFA_ERR_NOMEM);
+            if (hipMemcpy(*u.dst, u.src, u.bytes, hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
+        }
+        // scratch per kernel pair <= 128 MB so it stays in the 256 MB Infinity Cache
+        h->dit_frames = (int)std::max<size_t>(1, ((size_t)128 << 20) / ((size_t)n * sizeof(float2)));
     }
     if (rfa::wide_supported(logn)) {
         std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn, h->wide_big));
@@ -384,6 +468,11 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_window_black);
     hipFree(h->d_window_il);
     hipFree(h->d_wide_tw);
+    hipFree(h->d_dit_window);
+    hipFree(h->d_dit_black);
+    hipFree(h->d_dit_c);
+    hipFree(h->d_dit_d);
+    hipFree(h->d_dit_y);
     hipFree(h->d_twc);
     hipFree(h->d_twf);
     hipFree(h->d_ring);

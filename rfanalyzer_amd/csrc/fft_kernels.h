@@ -38,6 +38,10 @@ struct FftLaunch {
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
+    // decimation in time for N > 2^17 (wide kernel, complex out): with dit_ss = S > 1
+    // work item u is sub-frame (frame u / S, residue u % S) = samples S*m + u % S of a
+    // frame of S*M samples; window points at the [S][M] permuted window
+    int dit_ss = 0;
     int wide_big = 15;        // wide_logm() for N > 16 K (RFA_WIDE_LOGM)
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
@@ -57,6 +61,29 @@ constexpr int kWidePT = 32;  // wide kernel: points per thread (32 an
 inline int wide_logm(int logn, int big) { return logn <= 14 ? logn : big; }
 std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
+
+// N = 2^18 .. 2^20: decimation-in-time pair (DESIGN.md "Large N").  Kernel A is
+// the wide kernel on the S = N / 32768 strided sub-frames of each frame (complex
+// out to scratch); kernel B (dit_combine_kernel) forms
+// X[k + M s] = sum_r W_N^{r k} Y_r[k] W_S^{r s} per k and writes dB rows / ring
+// (or the ordered complex spectrum).
+struct DitLaunch {
+    const float2 *y = nullptr;   // scratch [n_frames][S][M]
+    int n_frames = 0;
+    int frame0 = 0;              // batch index of frame 0 (ring placement)
+    int logn = 0, logm = 15;
+    const float2 *tw_c = nullptr;  // [S][M/128]  W_N^{r * 128 * khi}
+    const float2 *tw_d = nullptr;  // [S][128]    W_N^{r * klo}
+    float *rows = nullptr;
+    float *ring = nullptr;
+    int ring_rows = 0, ring_base = 0, ring_first = 0;
+    float2 *complex_out = nullptr;
+    hipStream_t stream = nullptr;
+};
+constexpr int kDitLogM = 15;
+constexpr int kMaxLogN = 20;
+hipError_t launch_dit_combine(const DitLaunch &a);
+void dit_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at
 // rows + f*row_stride, or, when ring_rows > 0, at rows + ((ring_base - f) mod ring_rows)*n

@@ -424,23 +424,34 @@ __global__ void state_kernel(StateLaunch a) {
 //   w: the chunk's EMA started from -inf (= em_out whenever em_in is -inf or the
 //      chunk restarts: after a -inf frame both runs are identical).
 __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+    // 4 adjacent bins per thread: one 16-B row load per frame (N is a multiple of 64)
+    const int bin = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
     const int c = blockIdx.y;
     if (bin >= a.n) return;
     const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
     const float al = a.ema_alpha, keep = 1.0f - al;
-    float pk = -INFINITY, emi = -INFINITY, am = 1.0f, b = 0.0f;
-    bool restart = false;
-#pragma unroll 8
+    float pk[4], emi[4], b[4];
+    bool restart[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
+    float am = 1.0f;
+#pragma unroll 4
     for (int f = f0; f < f1; f++) {
-        const float x = state_row(a, f)[bin];
-        pk = fmaxf(pk, x);
-        emi = (emi > -INFINITY) ? emi + al * (x - emi) : x;
-        restart |= x == -INFINITY;
+        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float x = xs[k];
+            pk[k] = fmaxf(pk[k], x);
+            emi[k] = (emi[k] > -INFINITY) ? emi[k] + al * (x - emi[k]) : x;
+            restart[k] |= x == -INFINITY;
+            b[k] = b[k] + al * (x - b[k]);
+        }
         am *= keep;
-        b = b + al * (x - b);
     }
-    a.part[(size_t)c * a.n + bin] = make_float4(pk, restart ? -1.0f : am, b, emi);
+    float4 *out = a.part + (size_t)c * a.n + bin;
+#pragma unroll
+    for (int k = 0; k < 4; k++) out[k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
 }
 
 __global__ void state_combine_kernel(StateLaunch a, int chunks) {
@@ -465,7 +476,8 @@ hipError_t launch_state(const StateLaunch &a) {
     if (chunks > 1) {
         const int len = (a.n_frames + chunks - 1) / chunks;
         chunks = (a.n_frames + len - 1) / len;
-        hipLaunchKernelGGL(state_partial_kernel, dim3(bx, chunks), dim3(tpb), 0, a.stream, a, len);
+        hipLaunchKernelGGL(state_partial_kernel, dim3((a.n / 4 + tpb - 1) / tpb, chunks), dim3(tpb), 0, a.stream, a,
+                           len);
         hipLaunchKernelGGL(state_combine_kernel, dim3(bx), dim3(tpb), 0, a.stream, a, chunks);
     } else {
         hipLaunchKernelGGL(state_kernel, dim3(bx), dim3(tpb), 0, a.stream, a);

@@ -307,7 +307,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int tid = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::HALFP;
 
-    const int items = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int work = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
+    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
     // One work item (SLOTS frames, or one residue of a frame).  Between items no
@@ -320,9 +321,14 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         asm volatile("s_mov_b32 %0, 0" : "=s"(z));
         const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
         int frame, r;
+        int dit_r = 0;  // decimation-in-time residue (a.dit_ss > 1): sub-frame = (frame, dit_r)
         if constexpr (RS == 1) {
             frame = u * G::SLOTS + slot;
             r = 0;
+            if (COMPLEX_OUT && a.dit_ss > 1) {
+                dit_r = frame % a.dit_ss;
+                frame /= a.dit_ss;
+            }
         } else {
             // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
             const int g = u / (8 * RS), rem = u - g * (8 * RS);
@@ -330,18 +336,22 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             frame = g * 8 + (rem & 7);
         }
         const bool active = frame < a.n_frames;
+        // sample stride and full frame length (decimation in time: S and S*M)
+        const int ss = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.dit_ss : 1;
+        constexpr int SB0 = FMT == 4 ? 4 : BPS;
         // inactive slots read zeros (num_records = 0) and store nothing
-        const rsrc_t in_rs = make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride,
-                                       active ? (unsigned)(n * BPS) : 0u);
-        const int planar_im = n * 4;
+        const rsrc_t in_rs =
+            make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride + (size_t)dit_r * SB0,
+                      active ? (unsigned)(n * ss * BPS - dit_r * SB0) : 0u);
+        const int planar_im = n * ss * 4;
 
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
         if constexpr (RS == 1) {
             // all PT raw samples of the thread in flight at once (buffer loads need
             // no address registers), then the window (L2-resident) and convert.
-            const rsrc_t w_rs = make_rsrc(a.window, n * 4);
-            constexpr int SB = FMT == 4 ? 4 : BPS;
+            const rsrc_t w_rs = make_rsrc(a.window + (size_t)dit_r * n, n * 4);
+            const int SB = SB0 * ss;  // bytes between consecutive samples of this (sub-)frame
             typename Raw<FMT>::T raw[PT];
     #pragma unroll
             for (int idx = 0; idx < PT; idx++) {
@@ -381,7 +391,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if (!active) return;
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
         if constexpr (COMPLEX_OUT) {
-            const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * n, n * 8);
+            const rsrc_t o_rs = make_rsrc(a.complex_out + ((size_t)frame * ss + dit_r) * n, n * 8);
     #pragma unroll
             for (int b = 0; b < PT / G::R2; b++)
     #pragma unroll
@@ -446,7 +456,8 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int items = RS == 1 ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int work = (RS == 1 && CO && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
+    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;
     if (a.persist > 0) {  // persistent: a.persist workgroups per CU (grid a multiple of 8*RS)
@@ -465,6 +476,16 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
 template <int LOGM, int PT, int RS, bool CO>
 static hipError_t wide_by_fmt(const FftLaunch &a) {
     if constexpr (CO) {
+        if constexpr (LOGM == kDitLogM && RS == 1) {  // kernel A of the large-N path: every format
+            switch (a.fmt) {
+            case 0: return launch_wide_one<LOGM, PT, RS, 0, true>(a);
+            case 1: return launch_wide_one<LOGM, PT, RS, 1, true>(a);
+            case 2: return launch_wide_one<LOGM, PT, RS, 2, true>(a);
+            case 3: return launch_wide_one<LOGM, PT, RS, 3, true>(a);
+            case 4: return launch_wide_one<LOGM, PT, RS, 4, true>(a);
+            default: return hipErrorInvalidValue;
+            }
+        }
         return a.fmt == 3 ? launch_wide_one<LOGM, PT, RS, 3, true>(a) : hipErrorInvalidValue;
     } else {
         switch (a.fmt) {
@@ -521,6 +542,10 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         case 31: return launch_wide_one<14, 32, 1, 0, false, 31>(a);
         default: return hipErrorInvalidValue;
         }
+    }
+    if (a.dit_ss > 1) {  // kernel A of the large-N decimation-in-time path
+        if (!co) return hipErrorInvalidValue;
+        return wide_by_fmt<kDitLogM, 32, 1, true>(a);
     }
     if (a.logn >= 15 && a.wide_big == 15) {
         switch (a.logn) {

@@ -19,8 +19,6 @@ def _engine(rfa, n, fmt, window, **kw):
 
 @pytest.mark.parametrize("spec", FIXTURES, ids=[s["name"] for s in FIXTURES])
 def test_rows_match_reference_pffft_and_oracle(rfa, spec):
-    if spec["n"] > 131072:
-        pytest.skip("two-pass large-N path not built yet")
     data = gu.fixture_input(spec)
     with _engine(rfa, spec["n"], spec["fmt"], spec["window"], ring_rows=0) as e:
         rows = e.process(data, spec["n_frames"], spec.get("packet_size", 0))
@@ -32,7 +30,8 @@ def test_rows_match_reference_pffft_and_oracle(rfa, spec):
     assert gu.db_diff(rows, ref64) <= gu.DB_TOL
 
 
-@pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072])
+@pytest.mark.parametrize("n", [64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536, 131072,
+                               262144, 524288, 1048576])
 @pytest.mark.parametrize("fmt", ["s8", "u8", "s16", "f32", "f32p"])
 def test_all_sizes_and_formats_vs_oracle(rfa, n, fmt):
     frames = 3 if n <= 16384 else 1
@@ -128,4 +127,39 @@ def test_reference_seams_match_pffft(rfa):
     ref = oracle.ref_fft_ordered(inter)
     err = np.abs((cx[0::2] + 1j * cx[1::2]) - (ref[0::2] + 1j * ref[1::2])).max()
     assert err / np.abs(ref).max() < 1e-5
+    dsp.close()
+
+
+@pytest.mark.parametrize("n,frames", [(262144, 65), (1048576, 17)])
+def test_large_n_batches_cross_the_scratch_split(rfa, n, frames):
+    """N > 2^17 runs as two kernels over batches of 128 MB of scratch
+    (64 frames at 2^18, 16 at 2^20): a batch one frame longer crosses the split;
+    rows, ring and peak-hold must not see the seam."""
+    data = signals.frames_bytes(n, frames, "s8", n + 3, tones=((0.2113, 0.4),), noise=0.05, drift=2e-4)
+    ref = oracle.spectrum_rows(data, oracle.IN_S8, n, frames, None, oracle.WIN_BLACKMAN)
+    with _engine(rfa, n, "s8", "blackman", ring_rows=4, peak_hold=True) as e:
+        rows = e.process(data, frames)
+        ring, ri, wi = e.ring()
+        peaks = e.peaks()
+    assert gu.db_diff(rows, ref) <= gu.DB_TOL
+    gu.assert_same_peak_bins(rows, np.argmax(ref, 1))
+    assert gu.db_diff(ring[ri], ref[-1]) <= gu.DB_TOL  # newest row
+    assert gu.db_diff(peaks, ref.max(0)) <= gu.DB_TOL
+
+
+@pytest.mark.parametrize("n", [262144, 1048576])
+def test_large_n_seams(rfa, n):
+    """Reference seams at N > 2^17: ordered complex FFT vs float64, log-mag vs pffft."""
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(2 * n).astype(np.float32)
+    from rfanalyzer_amd.nativedsp import NativeDsp
+    dsp = NativeDsp()
+    cx = np.empty(2 * n, np.float32)
+    dsp.performFFT(x, cx)
+    ref = np.fft.fft(x[0::2].astype(np.float64) + 1j * x[1::2])
+    assert np.abs((cx[0::2] + 1j * cx[1::2]) - ref).max() / np.abs(ref).max() < 2e-6
+    if oracle.ref_available():
+        out = np.empty(n, np.float32)
+        dsp.performFFTAndLogMag(x, out)
+        assert gu.pffft_diff(out, oracle.ref_fft_logmag(x)) <= gu.DB_TOL
     dsp.close()
