@@ -142,6 +142,16 @@ RFA_API int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out);
 RFA_API int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_index);
 RFA_API int rfa_reset_state(rfa_handle *h); /* ring -> -9999, peaks/EMA -> uninitialised */
 
+/* Channel signal strength for the squelch (FftProcessor.kt:143-157): for every
+ * frame of each rfa_process batch, the mean dB over bins
+ * [((start - f0) * (N / sampleRate.toFloat())).toInt(), same for end), each
+ * clamped to [0, N], f0 = frequency - sampleRate / 2 (the tuning of
+ * rfa_set_tuning).  start_frequency == end_frequency disables it.
+ * rfa_get_channel_means copies the last batch's means in frame order
+ * (synchronises); *count = 0 when the channel range is empty. */
+RFA_API int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency);
+RFA_API int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, size_t *count);
+
 /* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers. */
 RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);
 

@@ -12,6 +12,7 @@ the FFT (paths relative to app/src/main/java/com/mantz_it/rfanalyzer/):
 * exponential average -- a north-star extension with the reference's only EMA
   idiom (database/GlobalPerformanceData.kt:44-50): first frame initialises,
   then avg += alpha*(x-avg); a -inf average is re-seeded by the next frame;
+* channel mean dB for the squelch (analyzer/FftProcessor.kt:143-157);
 * Scheduler framing of source packets into FFT frames
   (analyzer/Scheduler.kt:252-279, source/FileIQSource.java:318-369).
 """
@@ -144,3 +145,22 @@ def file_frames(n_bytes: int, packet_size: int, bytes_per_sample: int, n: int) -
         frames.append((p * packet_size, n))  # contiguous: whole packets concatenated
         p += per
     return frames
+
+
+def channel_mean(row: np.ndarray, n: int, frequency: int, sample_rate: int, start: int, end: int):
+    """FftProcessor.kt:143-157: mean dB over the channel's bins (None if empty).
+    Index math in float32 with Kotlin's truncating toInt(), coerceIn(0, N);
+    sequential float32 sum like the reference loop."""
+    samples_per_hz = np.float32(n) / np.float32(sample_rate)
+    f0 = frequency - sample_rate // 2
+
+    def idx(f):
+        return min(max(kotlin_float_to_int(np.float32(np.float32(f - f0) * samples_per_hz)), 0), n)
+
+    s, e = idx(start), idx(end)
+    if e <= s:
+        return None
+    acc = np.float32(0)
+    for v in np.asarray(row[s:e], np.float32):
+        acc = np.float32(acc + v)
+    return np.float32(acc / np.float32(e - s))

@@ -97,6 +97,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_get_kernel_time": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
         "rfa_main_kernel_name": (ctypes.c_char_p, [_h]),
         "rfa_retune_offset": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int64]),
+        "rfa_set_channel": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
+        "rfa_get_channel_means": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t,
+                                                 ctypes.POINTER(ctypes.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

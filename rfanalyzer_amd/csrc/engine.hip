@@ -57,6 +57,12 @@ struct rfa_handle {
     int state_chunks = 1;
     float *d_boxcar = nullptr;
     bool have_tuning = false;
+    // channel mean (FftProcessor.kt:143-157)
+    bool chan_on = false;
+    int64_t chan_start = 0, chan_end = 0;
+    float *d_chan = nullptr;
+    size_t d_chan_cap = 0;
+    size_t chan_count = 0;
     int64_t last_frequency = 0, last_sample_rate = 0;
     // staging for host-pointer entry points / state without a row buffer
     void *d_in = nullptr;
@@ -480,6 +486,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_peaks);
     hipFree(h->d_ema);
     hipFree(h->d_state_part);
+    hipFree(h->d_chan);
     hipFree(h->d_boxcar);
     hipFree(h->d_in);
     hipFree(h->d_rows);
@@ -534,11 +541,27 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     if (n_frames > (size_t)0x7fffffff) return fail(h, RFA_ERR_INVALID, "too many frames");
     if (n_frames == 0) return RFA_OK;
     const bool need_state = h->d_peaks || h->d_ema;
-    // state needs the rows of the whole batch: use the caller's, else the ring
-    // when every frame lands there, else a staging buffer
+    // channel mean bins of this tuning (FftProcessor.kt:143-151)
+    int chan_first = 0, chan_last = 0;
+    if (h->chan_on && h->have_tuning) {
+        const float samples_per_hz = (float)n / (float)h->last_sample_rate;
+        const int64_t f0 = h->last_frequency - h->last_sample_rate / 2;
+        auto idx = [&](int64_t f) {
+            const float x = (float)(f - f0) * samples_per_hz;
+            const long long i = std::isnan(x) ? 0 : x >= 2147483647.0f ? 2147483647LL : x <= -2147483648.0f ? -2147483648LL
+                                                                                                               : (long long)x;
+            return (int)std::min<long long>(std::max<long long>(i, 0), n);  // coerceIn(0, size)
+        };
+        chan_first = idx(h->chan_start);
+        chan_last = idx(h->chan_end);
+    }
+    const bool need_chan = chan_last > chan_first;
+    h->chan_count = 0;
+    // state and channel means need the rows of the whole batch: use the caller's,
+    // else the ring when every frame lands there, else a staging buffer
     float *state_rows = rows;
     bool rows_in_ring = false;
-    if (need_state && !rows) {
+    if ((need_state || need_chan) && !rows) {
         if (h->d_ring && n_frames <= (size_t)h->ring_rows) {
             rows_in_ring = true;
         } else {
@@ -562,7 +585,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     }
     int rc = launch_main(h, a);
     if (rc) return rc;
-    if (need_state) {
+    if (need_state || need_chan) {
         rfa::StateLaunch s;
         s.n = n;
         s.n_frames = (int)n_frames;
@@ -576,11 +599,16 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             s.rows = h->d_ring;
             s.ring_rows = h->ring_rows;
             s.ring_base = h->write_index;
-            HIPCHK(h, rfa::launch_state(s));
         } else {
             s.rows = state_rows;
             s.row_stride = n;
-            HIPCHK(h, rfa::launch_state(s));
+        }
+        if (need_state) HIPCHK(h, rfa::launch_state(s));
+        if (need_chan) {
+            rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, n_frames * sizeof(float));
+            if (rc) return rc;
+            HIPCHK(h, rfa::launch_channel_mean(s, chan_first, chan_last, h->d_chan));
+            h->chan_count = n_frames;
         }
     }
     if (h->d_ring) {
@@ -670,6 +698,25 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
         }
     }
     return reset_peaks_ema(h);  // FftProcessor.kt:238-239 (peaks), EMA likewise
+}
+
+int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency) {
+    if (!h) return RFA_ERR_INVALID;
+    h->chan_on = start_frequency != end_frequency;
+    h->chan_start = start_frequency;
+    h->chan_end = end_frequency;
+    return RFA_OK;
+}
+
+int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, size_t *count) {
+    if (!h || !count || (!out && capacity)) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    const size_t k = std::min(capacity, h->chan_count);
+    if (k) HIPCHK(h, hipMemcpyAsync(out, h->d_chan, k * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    *count = h->chan_count;
+    return RFA_OK;
 }
 
 int rfa_get_peaks(rfa_handle *h, float *out) {

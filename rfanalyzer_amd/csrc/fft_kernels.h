@@ -103,6 +103,8 @@ struct StateLaunch {
     hipStream_t stream = nullptr;
 };
 hipError_t launch_state(const StateLaunch &a);
+// Mean of row[first, last) for every frame (rows addressed as in StateLaunch).
+hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out);
 
 // Ring maintenance (FftProcessor.kt:197-220) and boxcar (AnalyzerSurface.kt:710-714).
 hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);

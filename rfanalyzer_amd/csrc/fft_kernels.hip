@@ -485,6 +485,26 @@ hipError_t launch_state(const StateLaunch &a) {
     return hipGetLastError();
 }
 
+// FftProcessor.kt:143-157: mean of the channel's dB bins, one workgroup per frame.
+__global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int first, int last, float *out) {
+    const int f = blockIdx.x;
+    const float *row = state_row(a, f);
+    float s = 0.0f;
+    for (int i = first + (int)threadIdx.x; i < last; i += 256) s += row[i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    __shared__ float part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[f] = (part[0] + part[1] + part[2] + part[3]) / (float)(last - first);
+}
+
+hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out) {
+    if (a.n_frames <= 0 || last <= first) return hipSuccess;
+    hipLaunchKernelGGL(channel_mean_kernel, dim3(a.n_frames), dim3(256), 0, a.stream, a, first, last, out);
+    return hipGetLastError();
+}
+
 __global__ void fill_kernel(float *p, long long count, float value) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
          i += (long long)gridDim.x * blockDim.x)

@@ -179,6 +179,19 @@ class SpectrumEngine:
     def set_profiling(self, on: bool) -> None:
         self._check(_lib.lib().rfa_set_profiling(self._h, 1 if on else 0), "rfa_set_profiling")
 
+    def set_channel(self, start_frequency: int, end_frequency: int) -> None:
+        """Channel range for the per-frame mean dB (FftProcessor.kt:143-157); equal ends disable it."""
+        self._check(_lib.lib().rfa_set_channel(self._h, int(start_frequency), int(end_frequency)), "rfa_set_channel")
+
+    def channel_means(self) -> np.ndarray:
+        """Per-frame channel mean dB of the last batch (empty when the channel range is empty)."""
+        cap = 1 << 16
+        out = np.empty(cap, np.float32)
+        cnt = ctypes.c_size_t()
+        self._check(_lib.lib().rfa_get_channel_means(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), cap,
+                                                     ctypes.byref(cnt)), "rfa_get_channel_means")
+        return out[:min(cnt.value, cap)].copy()
+
     def main_kernel_name(self) -> str:
         """HIP kernel that rfa_process launches for this configuration (rocprofv3 name)."""
         return _lib.lib().rfa_main_kernel_name(self._h).decode()

@@ -83,34 +83,20 @@ class FftProcessor:
     def process(self, frames, frequency: int, sample_rate: int, frame_stride: int = 0):
         """One batch of raw frames with common tuning -> rows (n_frames, N)."""
         t0 = time.perf_counter_ns()
+        rng = self.channel_range() if (self.channel_range and self.on_average_signal_strength) else None
+        self.engine.set_channel(*(rng if rng else (0, 0)))
         with self.data.lock:
             changed = frequency != self.data.frequency or sample_rate != self.data.sampleRate
             self.engine.set_tuning(frequency, sample_rate)
             rows = self.engine.process(frames, frame_stride=frame_stride)
             self.data.frequency, self.data.sampleRate = frequency, sample_rate
             self.data.frequencyOrSampleRateChanged = changed
-        if rows.shape[0]:
-            self._channel_average(rows[-1], frequency, sample_rate)
+        if rows.shape[0] and rng:
+            for mean in self.engine.channel_means():  # one value per frame, as the reference's per-frame callback
+                self.on_average_signal_strength(float(mean))
             ns_per_frame = self.n * 1e9 / sample_rate  # FftProcessor.kt:160-161
             self.perf.updateLoad("FftProcessor", (time.perf_counter_ns() - t0) / (ns_per_frame * rows.shape[0]))
         return rows
-
-    def _channel_average(self, row, frequency, sample_rate):
-        """FftProcessor.kt:143-157: mean dB over the channel's bins (squelch input)."""
-        if self.channel_range is None or self.on_average_signal_strength is None:
-            return
-        rng = self.channel_range()
-        if rng is None:
-            return
-        samples_per_hz = np.float32(self.n) / np.float32(sample_rate)
-        f0 = frequency - sample_rate // 2
-        start = int(np.clip(int(np.float32(rng[0] - f0) * samples_per_hz), 0, self.n))
-        end = int(np.clip(int(np.float32(rng[1] - f0) * samples_per_hz), 0, self.n))
-        if end > start:
-            acc = np.float32(0)
-            for v in row[start:end]:
-                acc = np.float32(acc + v)
-            self.on_average_signal_strength(float(acc / np.float32(end - start)))
 
     # -- thread form (FftProcessor.kt:84-96,106-123) --------------------------------
     def start(self) -> None:

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 import golden_util as gu
+import signals
 import oracle
 from oracle import processor
 
@@ -128,3 +129,25 @@ def test_chunked_state_with_silent_frames(rfa, batches):
     with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.3, ring_rows=0) as e:
         e.process(data[: (total - 1) * 2 * n], total - 1, rows=False)
         assert gu.db_diff(e.ema(), ema_before) <= gu.DB_TOL
+
+
+@pytest.mark.parametrize("n,freq,sr,chan", [(4096, 100_000_000, 2_000_000, (100_010_000, 100_060_000)),
+                                            (65536, 433_920_000, 20_000_000, (433_000_000, 434_500_000)),
+                                            (1024, 100_000_000, 2_000_000, (98_000_000, 99_500_000)),  # below: empty
+                                            (1024, 100_000_000, 2_000_000, (99_100_000, 103_000_000))])  # clamped
+def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
+    """FftProcessor.kt:143-157 squelch input: mean dB of the channel bins, every frame."""
+    frames = 12
+    data = signals.frames_bytes(n, frames, "s8", 17, tones=((0.01, 0.3), (-0.2, 0.05)), noise=0.05)
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, frames, None, oracle.WIN_BLACKMAN)
+    exp = [processor.channel_mean(r, n, freq, sr, *chan) for r in ref_rows]
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=8) as e:
+        e.set_tuning(freq, sr)
+        e.set_channel(*chan)
+        e.process(data, frames, rows=False)
+        got = e.channel_means()
+    if exp[0] is None:
+        assert got.size == 0
+        return
+    assert got.size == frames
+    np.testing.assert_allclose(got, np.array(exp, np.float32), rtol=0, atol=gu.DB_TOL)
