@@ -12,7 +12,8 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "librfa.so")
+# RFA_LIB: load an alternative build (A/B experiments, scripts/); default in-tree librfa.so
+LIB_PATH = os.environ.get("RFA_LIB") or os.path.join(HERE, "librfa.so")
 CSRC = os.path.join(HERE, "csrc")
 
 RFA_OK = 0

@@ -452,6 +452,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (h->d_peaks || h->d_ema) {
         // enough (bin, chunk) threads to fill the chip (~2^19) for large batches
         h->state_chunks = (int)std::min<size_t>(32, std::max<size_t>(1, ((size_t)1 << 19) / n));
+        if (const char *d = std::getenv("RFA_STATE_CHUNKS")) h->state_chunks = std::max(1, std::min(64, std::atoi(d)));
         if (h->state_chunks > 1 &&
             hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
             return bail(RFA_ERR_NOMEM);

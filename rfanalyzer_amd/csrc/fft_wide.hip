@@ -189,6 +189,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // are adjacent in the interleaved window (one 8/16-byte load).  Loads run one
 // chunk ahead of the arithmetic (software pipeline), so a wave keeps two
 // chunks of L2 requests in flight instead of waiting a full round trip per chunk.
+#ifndef PRE_DIST
+#define PRE_DIST 1
+#endif
 template <int LOGM, int PT, int RS, int FMT, int R>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im) {
@@ -207,12 +210,14 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
         for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, R * (M / 32) * 8);
     }
-    typename Raw<FMT>::T raw[2][C][RS];
-    float win[2][C][RS];
+    // loads run DIST chunks ahead of the arithmetic (RFA_PRE_DIST experiments: 1 or 2)
+    constexpr int DIST = PRE_DIST;
+    typename Raw<FMT>::T raw[DIST + 1][C][RS];
+    float win[DIST + 1][C][RS];
     // c is a template parameter throughout: every register array index below is a
     // compile-time constant (a runtime index would move the arrays to scratch)
     auto issue = [&]<int c>() {
-        constexpr int s = c & 1;
+        constexpr int s = c % (DIST + 1);
 #pragma unroll
         for (int q = 0; q < C; q++) {
             const int idx = c * C + q, b = idx >> 5, t = idx & 31;
@@ -238,7 +243,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
         }
     };
     auto compute = [&]<int c>() {
-        constexpr int s = c & 1;
+        constexpr int s = c % (DIST + 1);
         float2 accs[C];
 #pragma unroll
         for (int q = 0; q < C; q++) {
@@ -272,11 +277,13 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             }
         }
     };
-    issue.template operator()<0>();
+    [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+        ((Cs < DIST && Cs < NCH ? issue.template operator()<Cs>() : void()), ...);
+    }(std::make_integer_sequence<int, DIST>{});
     [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
         (
             [&] {
-                if constexpr (Cs + 1 < NCH) issue.template operator()<Cs + 1>();
+                if constexpr (Cs + DIST < NCH) issue.template operator()<Cs + DIST>();
                 __builtin_amdgcn_sched_barrier(0);
                 compute.template operator()<Cs>();
                 __builtin_amdgcn_sched_barrier(0);

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--samples", type=int, default=1 << 24, help="samples per launch")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--state", action="store_true", help="EMA + peak-hold + ring")
+    ap.add_argument("--no-prof", action="store_true", help="time steps without the per-launch HIP events")
     args = ap.parse_args()
     import torch
 
@@ -40,7 +41,7 @@ def main():
                 for k in range(3):
                     e.process_tensor(pools[k % 4], frames, 0, out)
                 torch.cuda.synchronize()
-                e.set_profiling(True)
+                e.set_profiling(not args.no_prof)
                 ms0, l0 = e.kernel_time()
                 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 ev0.record()
@@ -49,7 +50,7 @@ def main():
                 ev1.record()
                 torch.cuda.synchronize()
                 ms1, l1 = e.kernel_time()
-                kus = (ms1 - ms0) / (l1 - l0) * 1e3
+                kus = (ms1 - ms0) / (l1 - l0) * 1e3 if l1 > l0 else float("nan")
                 step_us = ev0.elapsed_time(ev1) / args.iters * 1e3
                 alg = frames * n * (BPS[fmt] + 4)
                 print(f"{fmt:5s} N={n:8d} frames={frames:6d} kernel {kus:9.1f} us  {alg / kus / 1e3:7.1f} GB/s  "
