@@ -19,6 +19,8 @@
 #include "../../include/rfa.h"
 #include "fft_kernels.h"
 
+static constexpr size_t kStampWords = (size_t)2048 * 16 * 8;  // RFA_STAMPS_FILE buffer: [blocks][16][8]
+
 using rfa::FftLaunch;
 
 struct rfa_handle {
@@ -42,6 +44,10 @@ struct rfa_handle {
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
+    int stage = 1;                    // RFA_STAGE: LDS-DMA staged input in the wide kernel
+    int pair = 0;                     // RFA_PAIR=1: 64 K staged kernel computes both residues per workgroup
+    std::string stamps_file;          // RFA_STAMPS_FILE (profiling only): phase stamps appended per launch
+    unsigned long long *d_stamps = nullptr;
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     int wide_big = 15;                // RFA_WIDE_LOGM: 15 (32 K workgroups) or 14 for N > 16 K
@@ -247,6 +253,12 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.diag = h->diag;
     a.persist = h->persist;
     a.stagger_ns = h->stagger_ns;
+    a.stage = h->stage;
+    a.pair = h->pair;
+    if (h->d_stamps) {
+        a.diag = 32;
+        a.stamps = h->d_stamps;
+    }
     a.wide_big = h->wide_big;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
@@ -279,6 +291,17 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         h->ev_pending.emplace_back(e0, e1);
     }
     if (e != hipSuccess) return hip_fail(h, e, "launch_fft");
+    if (a.stamps) {  // profiling only: synchronous dump of this launch's phase stamps
+        std::vector<unsigned long long> st((size_t)kStampWords);
+        if (hipMemcpyAsync(st.data(), a.stamps, st.size() * 8, hipMemcpyDeviceToHost, h->stream) == hipSuccess &&
+            hipStreamSynchronize(h->stream) == hipSuccess) {
+            if (FILE *f = std::fopen(h->stamps_file.c_str(), "ab")) {
+                std::fwrite(st.data(), 8, st.size(), f);
+                std::fclose(f);
+            }
+        }
+        hipMemsetAsync(a.stamps, 0, st.size() * 8, h->stream);
+    }
     return RFA_OK;
 }
 
@@ -423,6 +446,13 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
     if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
+    if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
+    if (const char *d = std::getenv("RFA_PAIR")) h->pair = std::atoi(d);
+    if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
+        h->stamps_file = d;
+        if (hipMalloc(&h->d_stamps, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMemset(h->d_stamps, 0, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_HIP);
+    }
     if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
@@ -470,6 +500,7 @@ int rfa_destroy(rfa_handle *h) {
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
+    hipFree(h->d_stamps);
     hipFree(h->d_window);
     hipFree(h->d_window_none);
     hipFree(h->d_window_black);

@@ -71,30 +71,55 @@ __device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
 // and the inputs with t' in [h*R'/2, (h+1)*R'/2), which come from the same
 // half.  Reads go to fresh SSA temporaries (compile-time renaming), so round-1
 // outputs are never overwritten by round-0 inputs.
-template <int Q, int LOGM, int PT>
-__device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
+// LDS pointer the compiler cannot see through: per-thread LDS bases built
+// inside a work item are then not hoisted out of the item loop (and spilled)
+// when registers are tight (PAIR kernel).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(3))) T *lds_opaque(T *p) {
+    auto q = (__attribute__((address_space(3))) T *)p;
+    asm volatile("" : "+v"(q));
+    return q;
+}
+#else
+template <typename T>
+__device__ __forceinline__ T *lds_opaque(T *p) { return p; }  // host pass: never executed
+#endif
+
+template <int Q, int LOGM, int PT, bool OPQ = false>
+__device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf0, int tid) {
     using G = WGeo<LOGM, PT>;
     using W = WPass<Q, LOGM, PT>;
     using N = WPass<Q + 1, LOGM, PT>;
     static_assert(N::R >= 2, "half-round split needs radix >= 2");
     float2 in[2][PT / 2];
     const int wk = tid & (W::P - 1);
-    const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
-    const int rbase = padw(tid);                     // butterfly b adds TPF*b
-    const int my_half = tid >= G::TPF / 2;           // NB == 1 writers only
+    const int wbase0 = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
+    const int rbase0 = padw(tid);                     // butterfly b adds TPF*b
+    const int my_half = tid >= G::TPF / 2;            // NB == 1 writers only
+    // OPQ: write / read through opaque per-thread bases (+ compile-time offsets)
+    auto wbuf = [&] {
+        if constexpr (OPQ) return lds_opaque(buf0 + wbase0);
+        else return buf0;
+    }();
+    auto rbuf = [&] {
+        if constexpr (OPQ) return lds_opaque(buf0 + rbase0);
+        else return buf0;
+    }();
+    const int wbase = OPQ ? 0 : wbase0, rbase = OPQ ? 0 : rbase0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         if constexpr (W::NB == 1) {
             if (my_half == h) {
 #pragma unroll
-                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
+                for (int t = 0; t < W::R; t++) wbuf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
             }
         } else {
 #pragma unroll
             for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
 #pragma unroll
                 for (int t = 0; t < W::R; t++)
-                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+                    wbuf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
             }
         }
         lds_barrier();
@@ -103,7 +128,7 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
 #pragma unroll
             for (int t = h * N::R / 2; t < (h + 1) * N::R / 2; t++)
                 in[h][b * (N::R / 2) + (t - h * N::R / 2)] =
-                    buf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
+                    rbuf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
         }
         lds_barrier();
     }
@@ -192,9 +217,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
-template <int LOGM, int PT, int RS, int FMT, int R>
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
-                                         int tid, int planar_im) {
+                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));  // bytes per sample (per plane)
@@ -202,6 +227,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     // fit beside the PT points in the register budget (64 VGPRs at PT = 32)
     constexpr int C = (PT == 64 ? 16 : 8) / RS > 0 ? (PT == 64 ? 16 : 8) / RS : 1;
     constexpr int NCH = PT / C;
+    auto lraw_t = [&] {  // this thread's samples in the staged frame (opaque base, see lds_opaque)
+        if constexpr (STG) return lds_opaque(lraw + tid);
+        else return lraw;
+    }();
     const rsrc_t w_rs = make_rsrc(window_il, M * RS * 4);
     const rsrc_t pa_rs = make_rsrc(wide_tw + G::TW_LDS, RS * (M / 32) * 8);
     const float2 *pre_b = wide_tw + G::TW_LDS + RS * (M / 32) + R * 32;
@@ -223,7 +252,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             const int idx = c * C + q, b = idx >> 5, t = idx & 31;
             const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
 #pragma unroll
-            for (int j = 0; j < RS; j++) raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
+            for (int j = 0; j < RS; j++) {
+                if constexpr (STG) raw[s][q][j] = lraw_t[mo + j * M];  // frame staged in LDS
+                else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
+            }
             if constexpr (RS == 2) {
                 const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
                 win[s][q][0] = w.x;
@@ -259,6 +291,19 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
                     ...);
             }(std::make_integer_sequence<int, RS>{});
         }
+        if constexpr (RS == 2 && R != 0) {
+            // W_N^{m R} = pre_a[tid + TPF b] * W_64^{t R} (N = 2M: pre_b is a compile-time
+            // rotation, no table reads / scalar address registers)
+            [&]<int... Qs>(std::integer_sequence<int, Qs...>) {
+                (
+                    [&] {
+                        constexpr int i0 = c * C + Qs;
+                        v[i0] = w64<((i0 & 31) * R) & 63>(cmul(accs[Qs], pa[i0 >> 5]));
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, C>{});
+            return;
+        }
         // twiddle W_N^{m R} = pre_a * pre_b, then acc * twiddle: independent pairs interleaved
 #pragma unroll
         for (int q = 0; q < C; q += 2) {
@@ -292,9 +337,48 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     }(std::make_integer_sequence<int, NCH>{});
 }
 
+// LDS-DMA staging of one frame's raw bytes (STG kernels): the frame's n*BPS
+// bytes go HBM -> LDS exchange buffer in natural order, 1 KiB per wave
+// instruction (buffer_load_dwordx4 ... lds: no VGPRs, 16 B per lane), issued
+// for the NEXT work item right after the current item's last LDS exchange, so
+// the loads fly during pass 2, the dB epilogue and the next item's start.
+template <int BYTES, int THREADS>
+__device__ __forceinline__ void stage_frame(const uint8_t *src, float2 *buf) {
+    static_assert(BYTES % (1024 * (THREADS / 64)) == 0, "whole 1 KiB pieces per wave");
+    constexpr int NW = THREADS / 64, PER = BYTES / 1024 / NW;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const rsrc_t rs = make_rsrc(src, BYTES);
+    // LDS byte address of the buffer (generic -> local address-space cast)
+    const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)(uint8_t *)buf;
+    // Inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: hipcc treats a pending
+    // LDS-DMA as aliasing every later ds_read and waits vmcnt(0) before pass 2's
+    // twiddle reads, which would serialise the prefetch.  Its completion is waited
+    // for explicitly (vmcnt(0) + barrier at the start of the next item).
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        const int c = j * NW + w;  // wave-uniform 1 KiB piece
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(base + c * 1024), "v"(lane * 16), "s"(rs), "s"(c * 1024)
+            : "memory");
+    }
+}
+
 // DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
 // 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
-template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0>
+// STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
+// formats, one sub-FFT per workgroup, frame fits the exchange buffer; the
+// host launches a persistent grid and checks 16-byte alignment).
+// PAIR (RS = 2, STG): one workgroup computes BOTH residues of a frame, one after
+// the other; residue 0's dB values wait in VGPRs and residue 1's epilogue stores
+// bins (2i, 2i+1) together, so every row/ring line is written whole by one
+// store (residues in separate workgroups store alternate dwords, which doubled
+// the HBM write traffic: profiles/r01k/pmc.json).
+template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false, bool PAIR = false>
 __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) fft_wide_kernel(FftLaunch a) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
@@ -315,13 +399,110 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     float2 *buf = data + slot * G::HALFP;
 
     const int work = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
-    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int items = PAIR ? a.n_frames : RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
+    static_assert(!PAIR || (RS == 2 && STG), "PAIR: two residues, staged input");
+
+    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~32) == 0 &&
+                           M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
+    // frame of work item u (same mapping as body())
+    auto frame_of = [&](int u) {
+        if constexpr (RS == 1 || PAIR) return u;
+        else return (u / (8 * RS)) * 8 + (u & 7);
+    };
+    if constexpr (STG) {
+        const int f0 = frame_of(blockIdx.x);
+        if ((int)blockIdx.x < items && f0 < a.n_frames)
+            stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
+    }
 
     // One work item (SLOTS frames, or one residue of a frame).  Between items no
     // extra barrier is needed: the last LDS reads of an item (exchange 1) are
     // followed by a barrier before anyone leaves the FFT.
-    auto body = [&](int u) {
+    // DIAG & 32 (profiling only): s_memrealtime stamps of each item's phases by
+    // thread 0 into a.stamps[block][item < 16][8] (engine: RFA_STAMPS_FILE)
+    auto stamp = [&](int u, int k) {
+        if constexpr ((DIAG & 32) != 0) {
+            const int it = (u - (int)blockIdx.x) / (int)gridDim.x;
+            if (threadIdx.x == 0 && it < 16)
+                a.stamps[((size_t)blockIdx.x * 16 + it) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+        }
+    };
+    auto pair_body = [&](int u, int unext) {
+        const int frame = u;
+        using RawT = typename Raw<FMT>::T;
+        const RawT *lraw = reinterpret_cast<const RawT *>(buf);
+        const rsrc_t none = make_rsrc(nullptr, 0);
+        float stash[PT];  // residue 0's dB values (bins 2i)
+        auto residue = [&]<int R>() {
+            // opaque zero per residue: keeps hipcc from carrying residue 0's twiddle
+            // reads over to residue 1 in registers
+            int z;
+            asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+            const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
+            stamp(u, R == 0 ? 0 : 7);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // staged frame landed
+            if constexpr (R == 0) stamp(u, 1);
+            float2 v[PT];
+            prestage<LOGM, PT, RS, FMT, R, true>(v, a.window_il, a.wide_tw, none, tid, 0, lraw);
+#pragma unroll
+            for (int b = 0; b < PT / 32; b++) dft<32>(&v[b * 32]);
+            if constexpr (R == 0) stamp(u, 2);
+            lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
+            exchange<0, LOGM, PT, true>(v, buf, tid);
+            if constexpr (R == 0) stamp(u, 3);
+            pass1<LOGM, PT>(v, tid, tp1);
+            exchange<1, LOGM, PT, true>(v, buf, tid);
+            if constexpr (R == 0) stamp(u, 4);
+            // buffer free: stage the frame again for residue 1 (an L2 hit), or the next frame
+            const int fs = R == 0 ? frame : frame_of(unext);
+            if (R == 0 || unext < items)
+                stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fs * (size_t)a.frame_stride, buf);
+            pass2<LOGM, PT>(v, tid, tp2);
+            if constexpr (R == 0) stamp(u, 5);
+            constexpr float db_off = -kDbPerLog2 * (float)(2 * (LOGM + 1));
+            if constexpr (R == 0) {
+#pragma unroll
+                for (int q = 0; q < PT; q++) stash[q] = db_unscaled(v[q], db_off);  // nativedsp.cpp:73-78
+            } else {
+                const bool to_ring = a.ring && frame >= a.ring_first;
+                int rr = 0;
+                if (to_ring) {
+                    rr = (a.ring_base - frame) % a.ring_rows;
+                    if (rr < 0) rr += a.ring_rows;
+                }
+                const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
+                const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
+                auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
+#pragma unroll
+                    for (int b = 0; b < PT / G::R2; b++) {
+#pragma unroll
+                        for (int t = 0; t < G::R2; t++) {
+                            const int q = b * G::R2 + t;
+                            const float2 pr = make_float2(stash[q], db_unscaled(v[q], db_off));
+                            // sub-bin i = tid + TPF b + t M/R2 -> bins 2i, 2i+1; fft-shift (nativedsp.cpp:77)
+                            // as a store offset, the lane part never wraps
+                            const int so = ((2 * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
+                            buf_store_f32x2(pr, rs0, tid * 8, so);
+                            if constexpr (decltype(both)::value) buf_store_f32x2(pr, rs1, tid * 8, so);
+                        }
+                    }
+                };
+                if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
+                else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
+                else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+                stamp(u, 6);
+            }
+        };
+        residue.template operator()<0>();
+        residue.template operator()<1>();
+    };
+    auto body = [&](int u, int unext) {
+        if constexpr (PAIR) {
+            pair_body(u, unext);
+            return;
+        }
+        stamp(u, 0);
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
         int z;
@@ -354,6 +535,14 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
 
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
+        using RawT = typename Raw<FMT>::T;
+        const RawT *lraw = reinterpret_cast<const RawT *>(buf);
+        if constexpr (STG) {
+            // this item's frame, staged by LDS-DMA during the previous item: wait for
+            // this wave's pieces, then for every wave's (the barrier)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            stamp(u, 1);
+        }
         if constexpr (RS == 1) {
             // all PT raw samples of the thread in flight at once (buffer loads need
             // no address registers), then the window (L2-resident) and convert.
@@ -364,6 +553,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             for (int idx = 0; idx < PT; idx++) {
                 const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
                 if constexpr (DIAG & 1) raw[idx] = synth_raw<FMT>(so + tid);
+                else if constexpr (STG) raw[idx] = lraw[so + tid];
                 else raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
             }
     #pragma unroll
@@ -378,7 +568,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs>(v, a.window_il, a.wide_tw, in_rs, tid, planar) : void()), ...);
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG>(v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw)
+                          : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
 
@@ -386,10 +577,22 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     #pragma unroll
         for (int b = 0; b < PT / 32; b++)
             if constexpr (!(DIAG & 4)) dft<32>(&v[b * 32]);
+        stamp(u, 2);
+        if constexpr (STG) lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
         if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT>(v, buf, tid);
+        stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
         if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT>(v, buf, tid);
+        stamp(u, 4);
+        if constexpr (STG) {
+            // exchange 1 ended with a barrier after its last reads: the buffer is free
+            // until the next item, so stage the next item's frame now
+            const int fn = frame_of(unext);
+            if (unext < items && fn < a.n_frames)
+                stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
+        }
         if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
+        stamp(u, 5);
         if constexpr ((DIAG & 12) != 0) {
     #pragma unroll
             for (int q = 0; q < PT; q++) asm volatile("" : "+v"(v[q].x), "+v"(v[q].y));
@@ -438,6 +641,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
             else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
             else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+            stamp(u, 6);
         }
     };
     if (a.stagger_ns > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
@@ -447,13 +651,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
             __builtin_amdgcn_s_sleep(32);
     }
-    for (int u = blockIdx.x; u < items; u += gridDim.x) body(u);
+    for (int u = blockIdx.x; u < items; u += gridDim.x) body(u, u + gridDim.x);
 }
 
-template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0>
+template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false, bool PAIR = false>
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
-    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG>;
+    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG, PAIR>;
     const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     static bool attr = false;
@@ -464,17 +668,20 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         attr = true;
     }
     const int work = (RS == 1 && CO && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
-    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int items = PAIR ? a.n_frames : RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;
-    if (a.persist > 0) {  // persistent: a.persist workgroups per CU (grid a multiple of 8*RS)
-        static int cus = 0;
+    if (a.persist > 0 || STG) {  // persistent: a.persist (STG: all resident) workgroups per CU
+        static int cus = 0, occ = 0;
         if (!cus) {
             int dev = 0;
             (void)hipGetDevice(&dev);
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(kern), G::THREADS,
+                                                             lds) != hipSuccess || occ < 1)
+                occ = 1;
         }
-        blocks = std::min(items, cus * a.persist);
+        blocks = std::min(items, cus * (a.persist > 0 ? a.persist : occ));
     }
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
     return hipGetLastError();
@@ -495,6 +702,23 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         }
         return a.fmt == 3 ? launch_wide_one<LOGM, PT, RS, 3, true>(a) : hipErrorInvalidValue;
     } else {
+        using G = WGeo<LOGM, PT>;
+        constexpr int M = 1 << LOGM;
+        // LDS-staged input: 16-byte aligned frames that fit the exchange buffer
+        const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
+        constexpr bool stg8 = G::SLOTS == 1 && M * RS * 2 <= G::HALFP * 8;
+        constexpr bool stg16 = G::SLOTS == 1 && M * RS * 4 <= G::HALFP * 8;
+        if constexpr (stg8 && RS == 2 && LOGM == 15) {
+            if (stg && a.pair && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true, true>(a);
+            if (stg && a.pair && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true, true>(a);
+        }
+        if constexpr (stg8) {
+            if (stg && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true>(a);
+            if (stg && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true>(a);
+        }
+        if constexpr (stg16) {
+            if (stg && a.fmt == 2) return launch_wide_one<LOGM, PT, RS, 2, false, 0, true>(a);
+        }
         switch (a.fmt) {
         case 0: return launch_wide_one<LOGM, PT, RS, 0, false>(a);
         case 1: return launch_wide_one<LOGM, PT, RS, 1, false>(a);
@@ -535,6 +759,17 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
 
 hipError_t launch_fft_wide(const FftLaunch &a) {
     const bool co = a.complex_out != nullptr;
+    if (a.diag == 32) {  // phase stamps of the staged s8 kernels (profiling only)
+        if (a.fmt != 0 || co || !a.stamps) return hipErrorInvalidValue;
+        switch (a.logn) {
+        case 13: return launch_wide_one<13, 32, 1, 0, false, 32, true>(a);
+        case 14: return launch_wide_one<14, 32, 1, 0, false, 32, true>(a);
+        case 15: return launch_wide_one<15, 32, 1, 0, false, 32, true>(a);
+        case 16: return a.pair ? launch_wide_one<15, 32, 2, 0, false, 32, true, true>(a)
+                               : launch_wide_one<15, 32, 2, 0, false, 32, true>(a);
+        default: return hipErrorInvalidValue;
+        }
+    }
     if (a.diag) {  // ablations: 16K, s8 only
         if (a.logn != 14 || a.fmt != 0 || co) return hipErrorInvalidValue;
         switch (a.diag) {
