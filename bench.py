@@ -37,7 +37,8 @@ def parse():
     p.add_argument("--fft-size", type=int, default=65536)
     p.add_argument("--format", default="s8", choices=list(BPS))
     p.add_argument("--window", default="blackman")
-    p.add_argument("--frames", type=int, default=256, help="frames per step (batch)")
+    p.add_argument("--frames", type=int, default=500,
+                   help="frames per step (batch); default one full waterfall ring (500 rows, FftProcessor.kt:103)")
     p.add_argument("--avg", default="ema", choices=["none", "ema", "boxcar"])
     p.add_argument("--ema-alpha", type=float, default=0.1)
     p.add_argument("--no-peak", action="store_true")

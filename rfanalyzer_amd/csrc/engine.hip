@@ -45,7 +45,6 @@ struct rfa_handle {
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
     int stage = 1;                    // RFA_STAGE: LDS-DMA staged input in the wide kernel
-    int pair = 0;                     // RFA_PAIR=1: 64 K staged kernel computes both residues per workgroup
     std::string stamps_file;          // RFA_STAMPS_FILE (profiling only): phase stamps appended per launch
     unsigned long long *d_stamps = nullptr;
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
@@ -254,7 +253,6 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.persist = h->persist;
     a.stagger_ns = h->stagger_ns;
     a.stage = h->stage;
-    a.pair = h->pair;
     if (h->d_stamps) {
         a.diag = 32;
         a.stamps = h->d_stamps;
@@ -447,7 +445,6 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
-    if (const char *d = std::getenv("RFA_PAIR")) h->pair = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
         h->stamps_file = d;
         if (hipMalloc(&h->d_stamps, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_NOMEM);

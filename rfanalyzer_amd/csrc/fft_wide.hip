@@ -72,8 +72,7 @@ __device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
 // half.  Reads go to fresh SSA temporaries (compile-time renaming), so round-1
 // outputs are never overwritten by round-0 inputs.
 // LDS pointer the compiler cannot see through: per-thread LDS bases built
-// inside a work item are then not hoisted out of the item loop (and spilled)
-// when registers are tight (PAIR kernel).
+// inside a work item are then not hoisted out of the item loop (and spilled).
 #if defined(__HIP_DEVICE_COMPILE__)
 template <typename T>
 __device__ __forceinline__ __attribute__((address_space(3))) T *lds_opaque(T *p) {
@@ -86,40 +85,30 @@ template <typename T>
 __device__ __forceinline__ T *lds_opaque(T *p) { return p; }  // host pass: never executed
 #endif
 
-template <int Q, int LOGM, int PT, bool OPQ = false>
-__device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf0, int tid) {
+template <int Q, int LOGM, int PT>
+__device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
     using G = WGeo<LOGM, PT>;
     using W = WPass<Q, LOGM, PT>;
     using N = WPass<Q + 1, LOGM, PT>;
     static_assert(N::R >= 2, "half-round split needs radix >= 2");
     float2 in[2][PT / 2];
     const int wk = tid & (W::P - 1);
-    const int wbase0 = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
-    const int rbase0 = padw(tid);                     // butterfly b adds TPF*b
-    const int my_half = tid >= G::TPF / 2;            // NB == 1 writers only
-    // OPQ: write / read through opaque per-thread bases (+ compile-time offsets)
-    auto wbuf = [&] {
-        if constexpr (OPQ) return lds_opaque(buf0 + wbase0);
-        else return buf0;
-    }();
-    auto rbuf = [&] {
-        if constexpr (OPQ) return lds_opaque(buf0 + rbase0);
-        else return buf0;
-    }();
-    const int wbase = OPQ ? 0 : wbase0, rbase = OPQ ? 0 : rbase0;
+    const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
+    const int rbase = padw(tid);                     // butterfly b adds TPF*b
+    const int my_half = tid >= G::TPF / 2;           // NB == 1 writers only
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         if constexpr (W::NB == 1) {
             if (my_half == h) {
 #pragma unroll
-                for (int t = 0; t < W::R; t++) wbuf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
+                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
             }
         } else {
 #pragma unroll
             for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
 #pragma unroll
                 for (int t = 0; t < W::R; t++)
-                    wbuf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
             }
         }
         lds_barrier();
@@ -128,7 +117,7 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf0, int tid)
 #pragma unroll
             for (int t = h * N::R / 2; t < (h + 1) * N::R / 2; t++)
                 in[h][b * (N::R / 2) + (t - h * N::R / 2)] =
-                    rbuf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
+                    buf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
         }
         lds_barrier();
     }
@@ -217,6 +206,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
+
 template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
@@ -343,7 +333,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 // for the NEXT work item right after the current item's last LDS exchange, so
 // the loads fly during pass 2, the dB epilogue and the next item's start.
 template <int BYTES, int THREADS>
-__device__ __forceinline__ void stage_frame(const uint8_t *src, float2 *buf) {
+__device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     static_assert(BYTES % (1024 * (THREADS / 64)) == 0, "whole 1 KiB pieces per wave");
     constexpr int NW = THREADS / 64, PER = BYTES / 1024 / NW;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -373,12 +363,7 @@ __device__ __forceinline__ void stage_frame(const uint8_t *src, float2 *buf) {
 // STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
 // formats, one sub-FFT per workgroup, frame fits the exchange buffer; the
 // host launches a persistent grid and checks 16-byte alignment).
-// PAIR (RS = 2, STG): one workgroup computes BOTH residues of a frame, one after
-// the other; residue 0's dB values wait in VGPRs and residue 1's epilogue stores
-// bins (2i, 2i+1) together, so every row/ring line is written whole by one
-// store (residues in separate workgroups store alternate dwords, which doubled
-// the HBM write traffic: profiles/r01k/pmc.json).
-template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false, bool PAIR = false>
+template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false>
 __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) fft_wide_kernel(FftLaunch a) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
@@ -399,20 +384,21 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     float2 *buf = data + slot * G::HALFP;
 
     const int work = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
-    const int items = PAIR ? a.n_frames : RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
-    static_assert(!PAIR || (RS == 2 && STG), "PAIR: two residues, staged input");
 
-    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~32) == 0 &&
+    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~96) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
-        if constexpr (RS == 1 || PAIR) return u;
+        if constexpr (RS == 1) return u;
         else return (u / (8 * RS)) * 8 + (u & 7);
     };
+    const int u0 = blockIdx.x;  // first item of this workgroup
+    auto next_item = [&](int u) { return u + (int)gridDim.x; };
     if constexpr (STG) {
-        const int f0 = frame_of(blockIdx.x);
-        if ((int)blockIdx.x < items && f0 < a.n_frames)
+        const int f0 = frame_of(u0);
+        if (u0 < items && f0 < a.n_frames)
             stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
     }
 
@@ -428,80 +414,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 a.stamps[((size_t)blockIdx.x * 16 + it) * 8 + k] = __builtin_amdgcn_s_memrealtime();
         }
     };
-    auto pair_body = [&](int u, int unext) {
-        const int frame = u;
-        using RawT = typename Raw<FMT>::T;
-        const RawT *lraw = reinterpret_cast<const RawT *>(buf);
-        const rsrc_t none = make_rsrc(nullptr, 0);
-        float stash[PT];  // residue 0's dB values (bins 2i)
-        auto residue = [&]<int R>() {
-            // opaque zero per residue: keeps hipcc from carrying residue 0's twiddle
-            // reads over to residue 1 in registers
-            int z;
-            asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-            const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
-            stamp(u, R == 0 ? 0 : 7);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");  // staged frame landed
-            if constexpr (R == 0) stamp(u, 1);
-            float2 v[PT];
-            prestage<LOGM, PT, RS, FMT, R, true>(v, a.window_il, a.wide_tw, none, tid, 0, lraw);
-#pragma unroll
-            for (int b = 0; b < PT / 32; b++) dft<32>(&v[b * 32]);
-            if constexpr (R == 0) stamp(u, 2);
-            lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
-            exchange<0, LOGM, PT, true>(v, buf, tid);
-            if constexpr (R == 0) stamp(u, 3);
-            pass1<LOGM, PT>(v, tid, tp1);
-            exchange<1, LOGM, PT, true>(v, buf, tid);
-            if constexpr (R == 0) stamp(u, 4);
-            // buffer free: stage the frame again for residue 1 (an L2 hit), or the next frame
-            const int fs = R == 0 ? frame : frame_of(unext);
-            if (R == 0 || unext < items)
-                stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fs * (size_t)a.frame_stride, buf);
-            pass2<LOGM, PT>(v, tid, tp2);
-            if constexpr (R == 0) stamp(u, 5);
-            constexpr float db_off = -kDbPerLog2 * (float)(2 * (LOGM + 1));
-            if constexpr (R == 0) {
-#pragma unroll
-                for (int q = 0; q < PT; q++) stash[q] = db_unscaled(v[q], db_off);  // nativedsp.cpp:73-78
-            } else {
-                const bool to_ring = a.ring && frame >= a.ring_first;
-                int rr = 0;
-                if (to_ring) {
-                    rr = (a.ring_base - frame) % a.ring_rows;
-                    if (rr < 0) rr += a.ring_rows;
-                }
-                const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
-                const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
-                auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
-#pragma unroll
-                    for (int b = 0; b < PT / G::R2; b++) {
-#pragma unroll
-                        for (int t = 0; t < G::R2; t++) {
-                            const int q = b * G::R2 + t;
-                            const float2 pr = make_float2(stash[q], db_unscaled(v[q], db_off));
-                            // sub-bin i = tid + TPF b + t M/R2 -> bins 2i, 2i+1; fft-shift (nativedsp.cpp:77)
-                            // as a store offset, the lane part never wraps
-                            const int so = ((2 * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
-                            buf_store_f32x2(pr, rs0, tid * 8, so);
-                            if constexpr (decltype(both)::value) buf_store_f32x2(pr, rs1, tid * 8, so);
-                        }
-                    }
-                };
-                if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
-                else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
-                else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
-                stamp(u, 6);
-            }
-        };
-        residue.template operator()<0>();
-        residue.template operator()<1>();
-    };
     auto body = [&](int u, int unext) {
-        if constexpr (PAIR) {
-            pair_body(u, unext);
-            return;
-        }
         stamp(u, 0);
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
@@ -618,7 +531,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             }
             const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
             const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
-            const int vo = (RS * tid + r) * 4;
+            // DIAG & 64 (profiling only): residue-major layout [r][i] instead of the
+            // interleaved bins -- same bytes, whole lines per workgroup (measures the
+            // cost of the partial-line stores)
+            const int vo = (DIAG & 64) ? tid * 4 : (RS * tid + r) * 4;
             // one uniform branch per item, not per store
             auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
     #pragma unroll
@@ -628,7 +544,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                         const float2 x = v[b * G::R2 + t];
                         const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
                         // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
-                        const int so = ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
+                        const int so = (DIAG & 64) ? (r * M + G::TPF * b + t * (M / G::R2)) * 4
+                                                   : ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
                         if constexpr (DIAG & 2) {
                             asm volatile("" ::"v"(db));
                         } else {
@@ -651,13 +568,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
             __builtin_amdgcn_s_sleep(32);
     }
-    for (int u = blockIdx.x; u < items; u += gridDim.x) body(u, u + gridDim.x);
+    for (int u = u0; u < items; u = next_item(u)) body(u, next_item(u));
 }
 
-template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false, bool PAIR = false>
+template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false>
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
-    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG, PAIR>;
+    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
     const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     static bool attr = false;
@@ -668,7 +585,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         attr = true;
     }
     const int work = (RS == 1 && CO && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
-    const int items = PAIR ? a.n_frames : RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
+    const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;
     if (a.persist > 0 || STG) {  // persistent: a.persist (STG: all resident) workgroups per CU
@@ -708,10 +625,6 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
         constexpr bool stg8 = G::SLOTS == 1 && M * RS * 2 <= G::HALFP * 8;
         constexpr bool stg16 = G::SLOTS == 1 && M * RS * 4 <= G::HALFP * 8;
-        if constexpr (stg8 && RS == 2 && LOGM == 15) {
-            if (stg && a.pair && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true, true>(a);
-            if (stg && a.pair && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true, true>(a);
-        }
         if constexpr (stg8) {
             if (stg && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true>(a);
             if (stg && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true>(a);
@@ -759,14 +672,17 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
 
 hipError_t launch_fft_wide(const FftLaunch &a) {
     const bool co = a.complex_out != nullptr;
+    if (a.diag == 64) {  // residue-major output layout (profiling only)
+        if (a.fmt != 0 || co || a.logn != 16) return hipErrorInvalidValue;
+        return launch_wide_one<15, 32, 2, 0, false, 64, true>(a);
+    }
     if (a.diag == 32) {  // phase stamps of the staged s8 kernels (profiling only)
         if (a.fmt != 0 || co || !a.stamps) return hipErrorInvalidValue;
         switch (a.logn) {
         case 13: return launch_wide_one<13, 32, 1, 0, false, 32, true>(a);
         case 14: return launch_wide_one<14, 32, 1, 0, false, 32, true>(a);
         case 15: return launch_wide_one<15, 32, 1, 0, false, 32, true>(a);
-        case 16: return a.pair ? launch_wide_one<15, 32, 2, 0, false, 32, true, true>(a)
-                               : launch_wide_one<15, 32, 2, 0, false, 32, true>(a);
+        case 16: return launch_wide_one<15, 32, 2, 0, false, 32, true>(a);
         default: return hipErrorInvalidValue;
         }
     }
