@@ -60,6 +60,7 @@ struct rfa_handle {
     float *d_ema = nullptr;
     float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
     int state_chunks = 1;
+    int state_fused = 1;              // RFA_STATE_FUSED=0: two-kernel chunked scan
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -478,8 +479,9 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (cfg->avg_mode == RFA_AVG_EMA && hipMalloc(&h->d_ema, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (h->d_peaks || h->d_ema) {
         // enough (bin, chunk) threads to fill the chip (~2^19) for large batches
-        h->state_chunks = (int)std::min<size_t>(32, std::max<size_t>(1, ((size_t)1 << 19) / n));
+        h->state_chunks = (int)std::min<size_t>(32, std::max<size_t>(1, ((size_t)1 << 20) / n));
         if (const char *d = std::getenv("RFA_STATE_CHUNKS")) h->state_chunks = std::max(1, std::min(64, std::atoi(d)));
+        if (const char *d = std::getenv("RFA_STATE_FUSED")) h->state_fused = std::atoi(d);
         if (h->state_chunks > 1 &&
             hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
             return bail(RFA_ERR_NOMEM);
@@ -623,6 +625,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         s.ema_alpha = h->cfg.ema_alpha;
         s.part = h->d_state_part;
         s.max_chunks = h->state_chunks;
+        s.fused = h->state_fused;
         s.stream = h->stream;
         if (rows_in_ring) {
             s.rows = h->d_ring;

@@ -102,6 +102,7 @@ struct StateLaunch {
     float ema_alpha = 0.f;
     float4 *part = nullptr;  // chunk summaries [max_chunks][n] (null: sequential kernel only)
     int max_chunks = 1;
+    int fused = 1;           // single-launch chunked scan (RFA_STATE_FUSED=0: partial + combine kernels)
     hipStream_t stream = nullptr;
 };
 hipError_t launch_state(const StateLaunch &a);

@@ -468,11 +468,70 @@ __global__ void state_combine_kernel(StateLaunch a, int chunks) {
     if (a.ema) a.ema[bin] = em;
 }
 
+// One launch for the chunked scan: a block owns 1024/CH bins (4 per thread) and
+// all CH chunks of frames; the chunk summaries meet in LDS and the block folds
+// them in frame order into peaks / EMA (same algebra as state_combine_kernel),
+// so no summary buffer round trip and no second launch.
+template <int CH>
+__global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chunk_len) {
+    constexpr int TPC = 256 / CH, BPB = 4 * TPC;  // threads per chunk, bins per block
+    __shared__ float4 part[CH][BPB];
+    const int c = threadIdx.x / TPC, l = threadIdx.x % TPC;
+    const int bin = blockIdx.x * BPB + 4 * l;
+    const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
+    const float al = a.ema_alpha, keep = 1.0f - al;
+    float pk[4], emi[4], b[4];
+    bool restart[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
+    float am = 1.0f;
+#pragma unroll 4
+    for (int f = f0; f < f1; f++) {
+        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);
+        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float x = xs[k];
+            pk[k] = fmaxf(pk[k], x);
+            emi[k] = (emi[k] > -INFINITY) ? emi[k] + al * (x - emi[k]) : x;
+            restart[k] |= x == -INFINITY;
+            b[k] = b[k] + al * (x - b[k]);
+        }
+        am *= keep;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < BPB; i += 256) {
+        const int gb = blockIdx.x * BPB + i;
+        float p = a.peaks ? a.peaks[gb] : 0.f;
+        float em = a.ema ? a.ema[gb] : 0.f;
+#pragma unroll
+        for (int cc = 0; cc < CH; cc++) {
+            const float4 q = part[cc][i];
+            p = fmaxf(p, q.x);
+            em = (em == -INFINITY || q.y < 0.0f) ? q.w : fmaf(q.y, em, q.z);
+        }
+        if (a.peaks) a.peaks[gb] = p;
+        if (a.ema) a.ema[gb] = em;
+    }
+}
+
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
     const int tpb = 256;
     const int bx = (a.n + tpb - 1) / tpb;
     int chunks = a.part ? std::min(a.max_chunks, (a.n_frames + 7) / 8) : 1;
+    if (chunks >= 8 && a.fused) {  // single-launch form: CH = 8, 16 or 32 chunks
+        const int ch = chunks >= 32 ? 32 : chunks >= 16 ? 16 : 8;
+        const int bpb = 1024 / ch;
+        if (a.n % bpb == 0) {
+            const int len = (a.n_frames + ch - 1) / ch;
+            auto k = ch == 32 ? state_fused_kernel<32> : ch == 16 ? state_fused_kernel<16> : state_fused_kernel<8>;
+            hipLaunchKernelGGL(k, dim3(a.n / bpb), dim3(256), 0, a.stream, a, len);
+            return hipGetLastError();
+        }
+    }
     if (chunks > 1) {
         const int len = (a.n_frames + chunks - 1) / chunks;
         chunks = (a.n_frames + len - 1) / len;
