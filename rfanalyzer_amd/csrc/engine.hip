@@ -45,6 +45,7 @@ struct rfa_handle {
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
     int stage = 1;                    // RFA_STAGE: LDS-DMA staged input in the wide kernel
+    unsigned *d_queue = nullptr;      // staged kernels' work-queue counters (RFA_DQ=1; default static items)
     std::string stamps_file;          // RFA_STAMPS_FILE (profiling only): phase stamps appended per launch
     unsigned long long *d_stamps = nullptr;
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
@@ -254,6 +255,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.persist = h->persist;
     a.stagger_ns = h->stagger_ns;
     a.stage = h->stage;
+    a.queue = h->d_queue;
     if (h->d_stamps) {
         a.diag = 32;
         a.stamps = h->d_stamps;
@@ -446,6 +448,15 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
+    {
+        // dynamic work queue for the staged one-residue kernels: off by default (it
+        // measured slower than the static stride with the current code)
+        const char *d = std::getenv("RFA_DQ");
+        if (d && std::atoi(d) != 0) {
+            if (hipMalloc(&h->d_queue, 16 * sizeof(unsigned)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+            if (hipMemset(h->d_queue, 0, 16 * sizeof(unsigned)) != hipSuccess) return bail(RFA_ERR_HIP);
+        }
+    }
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
         h->stamps_file = d;
         if (hipMalloc(&h->d_stamps, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_NOMEM);
@@ -500,6 +511,7 @@ int rfa_destroy(rfa_handle *h) {
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     hipFree(h->d_stamps);
+    hipFree(h->d_queue);
     hipFree(h->d_window);
     hipFree(h->d_window_none);
     hipFree(h->d_window_black);

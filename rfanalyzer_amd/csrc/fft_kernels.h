@@ -46,6 +46,9 @@ struct FftLaunch {
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
     int stage = 1;            // wide kernel: LDS-DMA staged 8/16-bit input when aligned (RFA_STAGE=0 disables)
+    // staged one-residue kernels: work-queue counter [0] + finisher count [1], zero at
+    // launch and zeroed again by the kernel's last workgroup (null = static item stride)
+    unsigned *queue = nullptr;
     int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
     int max_logm = 14;  // largest sub-FFT per workgroup (13 = experiment: 2 workgroups per CU)
     int diag = 0;  // ablation variant (profiling only): 1 no loads, 2 no stores, 4 no FFT passes, 32 stamps

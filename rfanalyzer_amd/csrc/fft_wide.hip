@@ -47,6 +47,8 @@ struct WGeo {
     static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
     static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
     static constexpr int LDS_BYTES = (TW_LDS + SLOTS * HALFP) * 8;
+    // staged kernels: + 16 B for the work-queue slot (next item index)
+    static constexpr int LDS_Q_BYTES = 16;
 };
 
 template <int Q, int LOGM, int PT>
@@ -207,7 +209,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #define PRE_DIST 1
 #endif
 
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false>
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
     using G = WGeo<LOGM, PT>;
@@ -246,7 +248,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
                 if constexpr (STG) raw[s][q][j] = lraw_t[mo + j * M];  // frame staged in LDS
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
-            if constexpr (RS == 2) {
+            if constexpr (NOWIN) {  // ablation (RFA_DIAG=16): constant window, no window loads
+#pragma unroll
+                for (int j = 0; j < RS; j++) win[s][q][j] = 1.0f / 128.0f;
+            } else if constexpr (RS == 2) {
                 const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
                 win[s][q][0] = w.x;
                 win[s][q][1] = w.y;
@@ -387,14 +392,41 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
-    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~96) == 0 &&
+    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~112) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
         if constexpr (RS == 1) return u;
         else return (u / (8 * RS)) * 8 + (u & 7);
     };
-    const int u0 = blockIdx.x;  // first item of this workgroup
+    // Work distribution.  Static: items blockIdx.x, +grid, ...  Dynamic (staged
+    // one-residue kernels with a.queue): every workgroup takes its next item from one
+    // device-wide counter a.queue[0], so workgroups that run slow take fewer items
+    // (8 K/16 K: -11 % kernel time).  The index of the next item travels to all waves
+    // through an LDS slot.  The last workgroup to finish (a.queue[1] counts
+    // finishers) zeroes both counters for the next launch.  Two-residue kernels keep
+    // the static stride: it puts the residues of a frame on one XCD (shared L2), which
+    // a single queue does not (+7 % at 64 K, measured).
+    const bool dq = STG && RS == 1 && a.queue != nullptr;
+    int *qslot = reinterpret_cast<int *>(data + G::SLOTS * G::HALFP);
+    auto dequeue = [&]() -> int {
+        const unsigned u = atomicAdd(a.queue, 1u);
+        return u < (unsigned)items ? (int)u : items;
+    };
+    if (a.stagger_ns > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
+        // the second half of the grid starts late so workgroups do not all stream HBM
+        // and compute in the same phases (speed only; RFA_STAGGER_NS)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+        while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
+            __builtin_amdgcn_s_sleep(32);
+    }
+    int u0 = blockIdx.x;  // first item of this workgroup
+    if (dq) {
+        if (threadIdx.x == 0) qslot[0] = dequeue();
+        __syncthreads();
+        u0 = qslot[0];
+        __syncthreads();  // every wave has read the slot before it is rewritten
+    }
     auto next_item = [&](int u) { return u + (int)gridDim.x; };
     if constexpr (STG) {
         const int f0 = frame_of(u0);
@@ -407,14 +439,19 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // followed by a barrier before anyone leaves the FFT.
     // DIAG & 32 (profiling only): s_memrealtime stamps of each item's phases by
     // thread 0 into a.stamps[block][item < 16][8] (engine: RFA_STAMPS_FILE)
+    int it_count = 0;  // items this workgroup has started (stamps)
     auto stamp = [&](int u, int k) {
         if constexpr ((DIAG & 32) != 0) {
-            const int it = (u - (int)blockIdx.x) / (int)gridDim.x;
+            const int it = it_count;
             if (threadIdx.x == 0 && it < 16)
                 a.stamps[((size_t)blockIdx.x * 16 + it) * 8 + k] = __builtin_amdgcn_s_memrealtime();
         }
     };
-    auto body = [&](int u, int unext) {
+    // stores the previous item's epilogue left in flight (STG: the wait for the
+    // staged frame skips them -- vmcnt counts in issue order and they are younger
+    // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
+    int pending_st = 0;
+    auto body = [&](int u, int &unext) {
         stamp(u, 0);
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
@@ -453,7 +490,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (STG) {
             // this item's frame, staged by LDS-DMA during the previous item: wait for
             // this wave's pieces, then for every wave's (the barrier)
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (pending_st >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (pending_st == 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             stamp(u, 1);
         }
         if constexpr (RS == 1) {
@@ -481,7 +520,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG>(v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw)
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0>(v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
@@ -491,7 +530,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         for (int b = 0; b < PT / 32; b++)
             if constexpr (!(DIAG & 4)) dft<32>(&v[b * 32]);
         stamp(u, 2);
-        if constexpr (STG) lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
+        if constexpr (STG) {
+            // dynamic queue: thread 0 takes the next item now; the barrier publishes it
+            if (dq && threadIdx.x == 0) qslot[0] = dequeue();
+            lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
+            if (dq) unext = qslot[0];
+        }
         if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT>(v, buf, tid);
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
@@ -555,27 +599,35 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                     }
                 }
             };
+            static_assert(!STG || PT == 32, "pending-store wait counts assume 32 stores per destination");
+            pending_st = (a.rows ? PT : 0) + (to_ring ? PT : 0);
             if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
             else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
             else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
             stamp(u, 6);
         }
     };
-    if (a.stagger_ns > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
-        // persistent grid: the second resident workgroup of a CU starts late so the
-        // two interleave memory and compute phases (speed only; RFA_STAGGER_NS)
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
-            __builtin_amdgcn_s_sleep(32);
+    for (int u = u0; u < items; it_count++) {
+        int un = dq ? items : next_item(u);  // with the queue, body() dequeues the next item into un
+        body(u, un);
+        u = un;
     }
-    for (int u = u0; u < items; u = next_item(u)) body(u, next_item(u));
+    if (dq) {
+        if (threadIdx.x == 0) {
+            __threadfence();  // this workgroup's dequeues are done before it counts itself finished
+            if (atomicAdd(a.queue + 1, 1u) == gridDim.x - 1) {  // last one out: reset for the next launch
+                atomicExch(a.queue, 0u);
+                atomicExch(a.queue + 1, 0u);
+            }
+        }
+    }
 }
 
 template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false>
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    const size_t lds = (size_t)G::LDS_BYTES;
+    const size_t lds = (size_t)G::LDS_BYTES + (STG ? G::LDS_Q_BYTES : 0);
     if (!a.wide_tw) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
@@ -600,7 +652,9 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         }
         blocks = std::min(items, cus * (a.persist > 0 ? a.persist : occ));
     }
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
+    FftLaunch b = a;
+    if (!STG) b.queue = nullptr;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, b);
     return hipGetLastError();
 }
 
@@ -672,6 +726,10 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
 
 hipError_t launch_fft_wide(const FftLaunch &a) {
     const bool co = a.complex_out != nullptr;
+    if (a.diag == 16 && a.logn == 16) {  // staged 64 K kernel without window loads (profiling only)
+        if (a.fmt != 0 || co) return hipErrorInvalidValue;
+        return launch_wide_one<15, 32, 2, 0, false, 16, true>(a);
+    }
     if (a.diag == 64) {  // residue-major output layout (profiling only)
         if (a.fmt != 0 || co || a.logn != 16) return hipErrorInvalidValue;
         return launch_wide_one<15, 32, 2, 0, false, 64, true>(a);

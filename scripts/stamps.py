@@ -15,7 +15,7 @@ li = int(sys.argv[2]) if len(sys.argv) > 2 else nl - 1
 s = d[li * W:(li + 1) * W].reshape(2048, 16, 8).astype(np.int64)
 valid = s[:, :, 0] > 0
 t0 = s[:, :, 0][valid].min()
-names = ["wait-staged", "load/convert/window", "pass0+xchg0", "pass1+xchg1", "pass2", "epilogue"]
+names = ["wait-staged", "load/convert/window+dft32", "barrier+xchg0", "pass1+xchg1", "pass2 (+DMA issue)", "epilogue"]
 print(f"launches {nl}, using {li}; blocks with items: {valid.any(1).sum()}, items: {valid.sum()}")
 for k in range(1, 7):
     a, b = s[:, :, k - 1], s[:, :, k]
@@ -24,7 +24,7 @@ for k in range(1, 7):
         continue
     dt = (b - a)[m] * 10e-3  # us
     print(f"{names[k-1]:22s} mean {dt.mean():7.2f} us  p10 {np.percentile(dt,10):7.2f}  p90 {np.percentile(dt,90):7.2f}")
-for it in range(4):
+for it in range(8):
     m = valid[:, it]
     if m.sum() == 0:
         break
