@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--ring-rows", type=int, default=500)
     p.add_argument("--pool-mib", type=int, default=768, help="input pool size (> Infinity Cache)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget (0 = skip)")
+    p.add_argument("--f32-steps", type=int, default=20, help="steps of the float32-input companion run (0 = skip)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -188,41 +189,50 @@ def main():
     import rfanalyzer_amd
 
     n, frames, fmt = args.fft_size, args.frames, args.format
-    eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
-                                        ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
-                                        ring_rows=args.ring_rows, device=local)
     stream = torch.cuda.Stream(device)  # a real stream shared by torch and librfa (not the null stream)
     torch.cuda.set_stream(stream)
-    eng.set_stream(stream.cuda_stream)
-    pool = make_pool(torch, n, frames, fmt, args.pool_mib, 3 + rank, device)
-    eng.set_tuning(100_000_000, 20_000_000)
 
-    def step(k):
-        eng.process_tensor(pool[k % len(pool)], frames, 0, None)
+    def run(fmt, steps, warmup, seed, sync_ranks):
+        """Warm up, then time `steps` rfa_process() steps of one batch each (barrier +
+        synchronize on both sides).  Returns (wall seconds, main-kernel ms per launch, kernel)."""
+        eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
+                                            ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
+                                            ring_rows=args.ring_rows, device=local)
+        eng.set_stream(stream.cuda_stream)
+        pool = make_pool(torch, n, frames, fmt, args.pool_mib, seed, device)
+        eng.set_tuning(100_000_000, 20_000_000)
 
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    eng.set_profiling(True)
-    ms0, l0 = eng.kernel_time()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    ms1, l1 = eng.kernel_time()
-    eng.set_profiling(False)
+        def step(k):
+            eng.process_tensor(pool[k % len(pool)], frames, 0, None)
+
+        for k in range(warmup):
+            step(k)
+        torch.cuda.synchronize()
+        if sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize()
+        eng.set_profiling(True)
+        ms0, l0 = eng.kernel_time()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(warmup + k)
+        torch.cuda.synchronize()
+        if sync_ranks:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        ms1, l1 = eng.kernel_time()
+        eng.set_profiling(False)
+        name = eng.main_kernel_name()
+        eng.close()
+        del pool
+        return elapsed, (ms1 - ms0) / max(1, l1 - l0), name
+
+    elapsed, kernel_ms, kernel_name = run(fmt, args.steps, args.warmup, 3 + rank, world > 1)
     elapsed = max_over_ranks(elapsed, world, device)
 
     samples = world * args.steps * frames * n
     msps = samples / elapsed / 1e6
-    kernel_ms = (ms1 - ms0) / max(1, l1 - l0)
     s_in = BPS[fmt]
     alg_bytes = frames * n * (s_in + 4)  # per main-kernel launch: raw IQ in + one fp32 row out
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
@@ -258,17 +268,26 @@ def main():
                    "parallelism": f"streams{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": eng.main_kernel_name(), "kernel_ms": round(kernel_ms, 4),
+                     "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
     }
     if rank == 0 and world == 1:
         result["roofline"]["copy_GBps"] = copy_ceiling(torch, device)
         result["roofline"]["frac_of_copy"] = round(achieved / result["roofline"]["copy_GBps"], 4)
+    if rank == 0 and world == 1 and fmt != "f32" and args.f32_steps > 0:
+        # BASELINE.json asks for 8-bit AND float32 IQ: the same workload on complex-float32
+        # input (12 B/sample algorithmic), reported beside the headline (never `value`)
+        el32, k32, _ = run("f32", args.f32_steps, args.warmup, 103, False)
+        alg32 = frames * n * (BPS["f32"] + 4)
+        result["f32"] = {"value": round(args.f32_steps * frames * n / el32 / 1e6, 2), "unit": "Msamples/s",
+                         "ms_per_step": round(el32 * 1e3 / args.f32_steps, 4), "kernel_ms": round(k32, 4),
+                         "roofline_achieved_GBps": round(alg32 / (k32 * 1e-3) / 1e9, 1),
+                         "roofline_frac": round(alg32 / (k32 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                         "alg_bytes_per_launch": alg32}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds, min(16, os.cpu_count() or 1))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

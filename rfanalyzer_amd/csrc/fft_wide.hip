@@ -337,6 +337,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 // instruction (buffer_load_dwordx4 ... lds: no VGPRs, 16 B per lane), issued
 // for the NEXT work item right after the current item's last LDS exchange, so
 // the loads fly during pass 2, the dB epilogue and the next item's start.
+// cache policy of the staging DMA (A/B builds: -DSTG_POLICY='"nt "')
+#ifndef STG_POLICY
+#define STG_POLICY ""
+#endif
 template <int BYTES, int THREADS>
 __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     static_assert(BYTES % (1024 * (THREADS / 64)) == 0, "whole 1 KiB pieces per wave");
@@ -356,7 +360,7 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
         unsigned keep;
         asm volatile(
             "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+            "buffer_load_dwordx4 %2, %3, %4 offen " STG_POLICY "lds\n\ts_mov_b32 m0, %0"
             : "=&s"(keep)
             : "s"(base + c * 1024), "v"(lane * 16), "s"(rs), "s"(c * 1024)
             : "memory");

@@ -2,6 +2,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_pre.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_pre.log; [ $rc -ge 124 ] && exit $rc
-timeout -k 10 200 python scripts/kbench.py --sizes 16384,32768,65536,131072 --formats s8,s16,f32 || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_pre.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_pre.log; [ $rc -ne 0 ] && exit $rc
+for d in 0 128 0 128; do echo "== DIAG $d"; RFA_DIAG=$d timeout -k 10 120 python scripts/kbench.py --sizes 65536 --formats s8 --iters 20 --samples 32768000 2>&1 | grep -v amdgpu.ids || exit 1; done
+bash scripts/exp_stamps.sh "65536" 32768000
