@@ -19,6 +19,8 @@
  *     analyzer/FftProcessor.kt:164-245                        rfa_get_ring(), rfa_get_peaks()
  *   AnalyzerSurface boxcar time average                    rfa_get_boxcar()
  *     ui/AnalyzerSurface.kt:657-714
+ *   AnalyzerSurface.drawPreprocessing (colour rows, path)  rfa_draw_preprocess()
+ *     ui/AnalyzerSurface.kt:599-743
  *   (north-star extension) exponential average             rfa_get_ema()
  *     idiom of database/GlobalPerformanceData.kt:44-50
  *
@@ -151,6 +153,37 @@ RFA_API int rfa_reset_state(rfa_handle *h); /* ring -> -9999, peaks/EMA -> unini
  * (synchronises); *count = 0 when the channel range is empty. */
 RFA_API int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency);
 RFA_API int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, size_t *count);
+
+/* Display preprocessing: the reference's
+ * AnalyzerSurface.drawPreprocessing (app/.../ui/AnalyzerSurface.kt:599-743)
+ * computed on the device from the ring, for the tuning of rfa_set_tuning and the
+ * newest row rfa_get_ring reports.  Every ring row is (re)computed (the
+ * reference refreshes dirty rows lazily; the result equals its colour buffer
+ * once every row has been refreshed).  Outputs (host, synchronous):
+ *   colors      [ring_rows][width] ARGB, ring storage order (colorBuffer[bufferIndex*width + i]):
+ *               colormap[clamp(((avg - min_db) * scale).toInt())] of the pixel's mean
+ *               bin value, black (0xff000000) outside the drawn range;
+ *   fft_path_y  [width]: fftHeight - (timeAverage - min_db) * dbWidth of the boxcar over
+ *               the newest average_length + 1 rows (the fftPath points), NaN where the
+ *               reference adds no point;
+ *   peaks_y     [width] or NULL: peaksYCoordinates (-1 outside), needs peak_hold;
+ *   autoscale   [2] or NULL: min / max of the time averages, starting from
+ *               (10, -100) = (VERTICAL_SCALE_UPPER_BOUNDARY, _LOWER_BOUNDARY), before
+ *               the reference's +-5 dB margin (AnalyzerSurface.kt:731-735).
+ * Bit-identical to the JVM's fp32 arithmetic; where the reference would index the
+ * row out of bounds (and throw) the bin is skipped. */
+typedef struct rfa_draw_params {
+    int32_t width;                /* surface width in pixels                           */
+    int32_t fft_height;           /* spectrum plot height in pixels                    */
+    int64_t viewport_frequency;   /* viewport centre frequency (Hz)                    */
+    int64_t viewport_sample_rate; /* viewport span (Hz)                                */
+    float min_db, max_db;         /* vertical scale (viewportVerticalScaleMin/Max)     */
+    int32_t average_length;       /* fftAverageLength, < ring_rows                     */
+    int32_t colormap_size;        /* entries of colormap                               */
+    const uint32_t *colormap;     /* ARGB colours, e.g. ColorMaps.kt createGqrxMap()   */
+} rfa_draw_params;
+RFA_API int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *colors, float *fft_path_y,
+                                float *peaks_y, float *autoscale);
 
 /* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers. */
 RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);

@@ -68,6 +68,14 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+class RfaDrawParams(ctypes.Structure):
+    """rfa_draw_params (include/rfa.h): AnalyzerSurface.drawPreprocessing inputs."""
+    _fields_ = [("width", ctypes.c_int32), ("fft_height", ctypes.c_int32),
+                ("viewport_frequency", ctypes.c_int64), ("viewport_sample_rate", ctypes.c_int64),
+                ("min_db", ctypes.c_float), ("max_db", ctypes.c_float), ("average_length", ctypes.c_int32),
+                ("colormap_size", ctypes.c_int32), ("colormap", ctypes.POINTER(ctypes.c_uint32))]
+
+
 def _declare(lib: ctypes.CDLL) -> None:
     sig = {
         "rfa_abi_version": (ctypes.c_int, []),
@@ -99,6 +107,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_main_kernel_name": (ctypes.c_char_p, [_h]),
         "rfa_retune_offset": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int64]),
         "rfa_set_channel": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
+        "rfa_draw_preprocess": (ctypes.c_int, [_h, ctypes.POINTER(RfaDrawParams), _vp, _fp, _fp, _fp]),
         "rfa_get_channel_means": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t,
                                                  ctypes.POINTER(ctypes.c_size_t)]),
     }

@@ -1,0 +1,125 @@
+// Display preprocessing on the device: the reference's
+// AnalyzerSurface.drawPreprocessing (app/.../ui/AnalyzerSurface.kt:599-743)
+// computed from the waterfall ring where it already lives, so a frame of the UI
+// needs width-sized rows back instead of N-float rows.
+//
+// Per ring row (newest first, rowNumber r -> bufferIndex (readIndex + r) % R) and
+// pixel i inside (firstPixel, lastPixel - 1): the mean of the row's bins
+// j in [(int)(i*spp), (i+1)*spp) (stopping at N), summed in bin order in fp32
+// (AnalyzerSurface.kt:693-705); the colour map index ((avg - minDB) * scale)
+// truncated and clamped (:721-722); black outside (:725).  Rows 0..L feed the
+// time average, summed newest first per pixel (:710-714), whose spectrum-path y
+// and autoscale min/max come from draw_finish_kernel; row 0 also gives the
+// peak-hold y (:707).  Every float operation is the reference's single fp32
+// operation in the reference's order (no FMA contraction), so the results are
+// bit-identical to the JVM's.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "fft_kernels.h"
+
+namespace rfa {
+
+#pragma clang fp contract(off)
+
+// Kotlin Float.toInt(): truncation, NaN -> 0, saturating.
+__device__ __forceinline__ int kt_toint(float x) {
+    if (x != x) return 0;
+    if (x >= 2147483648.0f) return 2147483647;
+    if (x <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)x;
+}
+
+// java.lang.Math.min / max on floats: NaN wins, -0 < +0.
+__device__ __forceinline__ float jmin(float a, float b) {
+    if (a != a || b != b) return NAN;
+    if (a == b) return signbit(a) ? a : b;
+    return a < b ? a : b;
+}
+__device__ __forceinline__ float jmax(float a, float b) {
+    if (a != a || b != b) return NAN;
+    if (a == b) return signbit(a) ? b : a;
+    return a > b ? a : b;
+}
+
+__global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int row_number = blockIdx.y;
+    if (i >= a.width) return;
+    const int buffer_index = (a.read_index + row_number) % a.ring_rows;
+    const float *row = a.ring + (size_t)buffer_index * a.n;
+    unsigned *out = a.colors + (size_t)buffer_index * a.width + i;
+    if (i >= a.first_pixel + 1 && i < a.last_pixel - 1) {
+        const bool peaks_here = row_number == 0 && a.peaks_y;
+        float avg = 0.0f, peak_avg = 0.0f;
+        int counter = 0;
+        const float hi = (float)(i + 1) * a.samples_per_px;
+        // (the reference reads fftRow[j + start] unchecked; a negative index -- which
+        // would throw there -- is skipped here instead of read)
+        int j = kt_toint((float)i * a.samples_per_px);
+        if (j + a.start < 0) j = -a.start;
+        for (; (float)j < hi && j + a.start < a.n; j++) {
+            avg += row[j + a.start];
+            if (peaks_here) peak_avg += a.peaks[j + a.start];
+            counter++;
+        }
+        avg = avg / (float)counter;
+        if (peaks_here) {
+            const float pk = peak_avg / (float)counter;
+            a.peaks_y[i] = (float)a.fft_height - (pk - a.min_db) * a.db_width;
+        }
+        if (row_number <= a.avg_length) a.avg_rows[(size_t)row_number * a.width + i] = avg;
+        int ci = kt_toint((avg - a.min_db) * a.scale);
+        ci = ci < 0 ? 0 : (ci >= a.colormap_size ? a.colormap_size - 1 : ci);
+        *out = a.colormap[ci];
+    } else {
+        *out = 0xff000000u;  // Color.rgb(0, 0, 0)
+        if (row_number == 0 && a.peaks_y) a.peaks_y[i] = -1.0f;
+    }
+}
+
+// Time average of rows 0..L per pixel (newest first), spectrum-path y, autoscale
+// min/max starting from (VERTICAL_SCALE_UPPER_BOUNDARY, _LOWER_BOUNDARY) =
+// (10, -100) (AppStateRepository.kt:92-93).  One workgroup; path y is NaN where
+// the reference adds no path point.
+__global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
+    __shared__ float smin[1024], smax[1024];
+    float mn = 10.0f, mx = -100.0f;
+    for (int i = threadIdx.x; i < a.width; i += blockDim.x) {
+        if (i >= a.first_pixel + 1 && i < a.last_pixel - 1) {
+            float acc = 0.0f;
+            for (int r = 0; r <= a.avg_length; r++) acc += a.avg_rows[(size_t)r * a.width + i];
+            const float ta = acc / (float)(a.avg_length + 1);
+            a.path_y[i] = (float)a.fft_height - (ta - a.min_db) * a.db_width;
+            mn = jmin(ta, mn);
+            mx = jmax(ta, mx);
+        } else {
+            a.path_y[i] = NAN;
+        }
+    }
+    // min / max are order independent (NaN propagates either way)
+    smin[threadIdx.x] = mn;
+    smax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            smin[threadIdx.x] = jmin(smin[threadIdx.x], smin[threadIdx.x + s]);
+            smax[threadIdx.x] = jmax(smax[threadIdx.x], smax[threadIdx.x + s]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        a.autoscale[0] = smin[0];
+        a.autoscale[1] = smax[0];
+    }
+}
+
+hipError_t launch_draw(const DrawLaunch &a) {
+    if (a.width <= 0 || a.ring_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(draw_rows_kernel, dim3((a.width + 255) / 256, a.ring_rows), dim3(256), 0, a.stream, a);
+    hipLaunchKernelGGL(draw_finish_kernel, dim3(1), dim3(1024), 0, a.stream, a);
+    return hipGetLastError();
+}
+
+}  // namespace rfa

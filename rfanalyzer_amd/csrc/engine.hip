@@ -69,6 +69,8 @@ struct rfa_handle {
     int64_t chan_start = 0, chan_end = 0;
     float *d_chan = nullptr;
     size_t d_chan_cap = 0;
+    void *d_draw = nullptr;           // rfa_draw_preprocess: colormap, colours, averages, outputs
+    size_t d_draw_cap = 0;
     size_t chan_count = 0;
     int64_t last_frequency = 0, last_sample_rate = 0;
     // staging for host-pointer entry points / state without a row buffer
@@ -530,6 +532,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_ema);
     hipFree(h->d_state_part);
     hipFree(h->d_chan);
+    hipFree(h->d_draw);
     hipFree(h->d_boxcar);
     hipFree(h->d_in);
     hipFree(h->d_rows);
@@ -742,6 +745,79 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
         }
     }
     return reset_peaks_ema(h);  // FftProcessor.kt:238-239 (peaks), EMA likewise
+}
+
+// Kotlin Double.toInt() / Float.toInt(): truncation toward zero, NaN -> 0, saturating.
+static int kt_toint(double x) {
+    if (std::isnan(x)) return 0;
+    if (x >= 2147483647.0) return 2147483647;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int)x;
+}
+
+int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *colors, float *fft_path_y, float *peaks_y,
+                        float *autoscale) {
+    if (!h || !p || !colors || !fft_path_y || !p->colormap) return RFA_ERR_INVALID;
+    if (p->width <= 0 || p->fft_height < 0 || p->colormap_size <= 0 || p->average_length < 0) return RFA_ERR_INVALID;
+    if (!h->d_ring) return fail(h, RFA_ERR_STATE, "display preprocessing reads the ring (ring_rows > 0)");
+    if (!h->have_tuning) return fail(h, RFA_ERR_STATE, "display preprocessing needs rfa_set_tuning (frequency, rate)");
+    if (p->average_length >= h->ring_rows) return RFA_ERR_INVALID;
+    if (peaks_y && !h->d_peaks) return fail(h, RFA_ERR_STATE, "peak-hold y needs peak_hold");
+    int rc = set_device(h);
+    if (rc) return rc;
+    const int n = h->n, R = h->ring_rows, W = p->width, L = p->average_length;
+    // AnalyzerSurface.kt:650-672, in the reference's types (Long, Double, Float, Int)
+    const float samples_per_hz = (float)n / (float)h->last_sample_rate;
+    const int64_t frequency_diff = p->viewport_frequency - h->last_frequency;
+    const int64_t sample_rate_diff = p->viewport_sample_rate - h->last_sample_rate;
+    const int start = kt_toint(((double)frequency_diff - (double)sample_rate_diff / 2.0) * (double)samples_per_hz);
+    const int end = n + kt_toint(((double)frequency_diff + (double)sample_rate_diff / 2.0) * (double)samples_per_hz);
+    rfa::DrawLaunch a;
+    a.samples_per_px = (float)(end - start) / (float)W;
+    const float db_diff = p->max_db - p->min_db;
+    a.db_width = (float)p->fft_height / db_diff;
+    a.scale = (float)p->colormap_size / db_diff;
+    a.first_pixel = start >= 0 ? 0 : kt_toint((double)((float)(start * -1) / a.samples_per_px));
+    a.last_pixel = end >= n ? kt_toint((double)((float)(n - start) / a.samples_per_px))
+                            : kt_toint((double)((float)(end - start) / a.samples_per_px));
+    a.start = start;
+    a.min_db = p->min_db;
+    a.ring = h->d_ring;
+    a.peaks = peaks_y ? h->d_peaks : nullptr;
+    a.ring_rows = R;
+    a.n = n;
+    a.read_index = h->read_index;
+    a.width = W;
+    a.fft_height = p->fft_height;
+    a.avg_length = L;
+    a.colormap_size = p->colormap_size;
+    // one device block: colormap | colours [R][W] | averages [L+1][W] | path y | peaks y | autoscale
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_cmap = al((size_t)p->colormap_size * 4), b_col = al((size_t)R * W * 4),
+                 b_avg = al((size_t)(L + 1) * W * 4), b_w = al((size_t)W * 4);
+    rc = ensure_device_buffer(h, &h->d_draw, &h->d_draw_cap, b_cmap + b_col + b_avg + 2 * b_w + 256);
+    if (rc) return rc;
+    char *base = static_cast<char *>(h->d_draw);
+    a.colormap = reinterpret_cast<const unsigned *>(base);
+    a.colors = reinterpret_cast<unsigned *>(base + b_cmap);
+    a.avg_rows = reinterpret_cast<float *>(base + b_cmap + b_col);
+    a.path_y = reinterpret_cast<float *>(base + b_cmap + b_col + b_avg);
+    a.peaks_y = peaks_y ? reinterpret_cast<float *>(base + b_cmap + b_col + b_avg + b_w) : nullptr;
+    a.autoscale = reinterpret_cast<float *>(base + b_cmap + b_col + b_avg + 2 * b_w);
+    a.stream = h->stream;
+    HIPCHK(h, hipMemcpyAsync(base, p->colormap, (size_t)p->colormap_size * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, rfa::launch_draw(a));
+    HIPCHK(h, hipMemcpyAsync(colors, a.colors, (size_t)R * W * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(fft_path_y, a.path_y, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));
+    if (peaks_y) HIPCHK(h, hipMemcpyAsync(peaks_y, a.peaks_y, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));
+    float mm[2];
+    HIPCHK(h, hipMemcpyAsync(mm, a.autoscale, 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (autoscale) {
+        autoscale[0] = mm[0];
+        autoscale[1] = mm[1];
+    }
+    return RFA_OK;
 }
 
 int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency) {

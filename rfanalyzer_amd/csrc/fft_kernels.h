@@ -112,6 +112,26 @@ hipError_t launch_state(const StateLaunch &a);
 // Mean of row[first, last) for every frame (rows addressed as in StateLaunch).
 hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out);
 
+// Display preprocessing (AnalyzerSurface.kt:599-743), display.hip.  Scalars are
+// computed on the host exactly as the reference does (double / fp32 / Kotlin toInt).
+struct DrawLaunch {
+    const float *ring = nullptr;   // [ring_rows][n]
+    const float *peaks = nullptr;  // [n] or null
+    int ring_rows = 0, n = 0, read_index = 0;
+    int width = 0, fft_height = 0, avg_length = 0;
+    int start = 0, first_pixel = 0, last_pixel = 0;
+    float samples_per_px = 0.f, min_db = 0.f, db_width = 0.f, scale = 0.f;
+    const unsigned *colormap = nullptr;
+    int colormap_size = 0;
+    unsigned *colors = nullptr;    // [ring_rows][width], ring storage order
+    float *avg_rows = nullptr;     // scratch [avg_length + 1][width]
+    float *path_y = nullptr;       // [width]
+    float *peaks_y = nullptr;      // [width] or null
+    float *autoscale = nullptr;    // [2]
+    hipStream_t stream = nullptr;
+};
+hipError_t launch_draw(const DrawLaunch &a);
+
 // Ring maintenance (FftProcessor.kt:197-220) and boxcar (AnalyzerSurface.kt:710-714).
 hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);
 hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s);

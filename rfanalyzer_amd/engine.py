@@ -192,6 +192,26 @@ class SpectrumEngine:
                                                      ctypes.byref(cnt)), "rfa_get_channel_means")
         return out[:min(cnt.value, cap)].copy()
 
+    def draw_preprocess(self, width: int, fft_height: int, viewport_frequency: int, viewport_sample_rate: int,
+                        min_db: float, max_db: float, average_length: int, colormap, peaks: bool = False):
+        """AnalyzerSurface.drawPreprocessing (AnalyzerSurface.kt:599-743) on the device, from the ring.
+
+        Returns (colors [ring_rows][width] uint32 ARGB in ring storage order,
+        fft_path_y [width] (NaN where no path point), peaks_y [width] or None,
+        (autoscale_min, autoscale_max))."""
+        cmap = np.ascontiguousarray(colormap, dtype=np.uint32)
+        p = _lib.RfaDrawParams(int(width), int(fft_height), int(viewport_frequency), int(viewport_sample_rate),
+                               float(min_db), float(max_db), int(average_length), int(cmap.size),
+                               cmap.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        colors = np.empty((self.cfg.ring_rows, int(width)), np.uint32)
+        path = np.empty(int(width), np.float32)
+        pk = np.empty(int(width), np.float32) if peaks else None
+        mm = np.empty(2, np.float32)
+        self._check(_lib.lib().rfa_draw_preprocess(self._h, ctypes.byref(p), colors.ctypes.data, _fptr(path),
+                                                   _fptr(pk) if pk is not None else None, _fptr(mm)),
+                    "rfa_draw_preprocess")
+        return colors, path, pk, (float(mm[0]), float(mm[1]))
+
     def main_kernel_name(self) -> str:
         """HIP kernel that rfa_process launches for this configuration (rocprofv3 name)."""
         return _lib.lib().rfa_main_kernel_name(self._h).decode()

@@ -1,0 +1,69 @@
+"""GPU: display preprocessing on the device (rfa_draw_preprocess, SURVEY.md §8(f)
+row 1) vs the restatement of AnalyzerSurface.drawPreprocessing
+(oracle/display.py) on the ring the device holds -- bit-exact: colours, path y,
+peak-hold y and autoscale min / max."""
+import numpy as np
+import pytest
+
+import signals
+from oracle import display as od
+
+pytestmark = pytest.mark.gpu
+
+N, R, F0, SR = 2048, 12, 100_000_000, 2_000_000
+
+
+def _engine(rfa, frames):
+    e = rfa.SpectrumEngine(N, "blackman", "s8", avg="none", peak_hold=True, ring_rows=R)
+    e.set_tuning(F0, SR)
+    data = signals.frames_bytes(N, frames, "s8", seed=21, tones=((0.13, 0.4), (0.31, 0.02)), noise=0.03)
+    e.process(data, frames, rows=False)
+    return e
+
+
+def _both(e, **kw):
+    ring, ri, _ = e.ring()
+    args = dict(width=333, fft_height=480, viewport_frequency=F0, viewport_sample_rate=SR, min_db=-110.0,
+                max_db=-20.0, average_length=3, colormap=od.gqrx_colormap())
+    args.update(kw)
+    got = e.draw_preprocess(peaks=True, **args)
+    exp = od.draw_preprocess(ring, ri, e.peaks(), F0, SR, **args)
+    return got, exp
+
+
+def _assert_same(got, exp):
+    colors, path, pk, mm = got
+    c2, p2, k2, mm2 = exp
+    np.testing.assert_array_equal(colors, c2)
+    assert np.array_equal(np.isnan(path), np.isnan(p2))
+    np.testing.assert_array_equal(path[~np.isnan(path)], p2[~np.isnan(p2)])
+    np.testing.assert_array_equal(pk, k2)
+    assert mm == mm2
+
+
+@pytest.mark.parametrize("vf,vsr", [(F0, SR), (F0 + 150_000, SR // 3), (F0, 2 * SR), (F0 - 700_000, SR),
+                                    (F0 + 333_333, 5 * SR // 4)])
+def test_viewports_bit_exact(rfa, vf, vsr):
+    e = _engine(rfa, 20)  # more frames than rows: the ring wrapped
+    try:
+        _assert_same(*_both(e, viewport_frequency=vf, viewport_sample_rate=vsr))
+    finally:
+        e.close()
+
+
+def test_partial_ring_and_no_average(rfa):
+    e = _engine(rfa, 5)  # rows 5..11 still hold the -9999 fill
+    try:
+        _assert_same(*_both(e, average_length=0, width=1000))
+        _assert_same(*_both(e, average_length=R - 1, min_db=-150.0, max_db=0.0))
+    finally:
+        e.close()
+
+
+def test_argument_checks(rfa):
+    e = _engine(rfa, 3)
+    try:
+        with pytest.raises(rfa.RfaError):
+            e.draw_preprocess(100, 100, F0, SR, -100, 0, R, od.gqrx_colormap())  # average_length >= ring rows
+    finally:
+        e.close()
