@@ -21,6 +21,8 @@
  *     ui/AnalyzerSurface.kt:657-714
  *   AnalyzerSurface.drawPreprocessing (colour rows, path)  rfa_draw_preprocess()
  *     ui/AnalyzerSurface.kt:599-743
+ *   MainViewModel scanner / squelch row reductions          rfa_row_window_stats()
+ *     ui/MainViewModel.kt:861-929,1391-1540
  *   (north-star extension) exponential average             rfa_get_ema()
  *     idiom of database/GlobalPerformanceData.kt:44-50
  *
@@ -184,6 +186,18 @@ typedef struct rfa_draw_params {
 } rfa_draw_params;
 RFA_API int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *colors, float *fft_path_y,
                                 float *peaks_y, float *autoscale);
+
+/* Scanner / squelch reductions of the newest ring row:
+ * for each inclusive bin window [lo[i], hi[i]] of the fft-shifted newest row
+ * (FftProcessorData.readIndex), peak = FloatArray.maxOrNull() (NaN wins) and
+ * avg = FloatArray.average().toFloat() (double sum / count).  Replaces the JVM
+ * loops of MainViewModel.kt:861-929 (detectIEMChannelsInFFT, window
+ * +-max(5, (100000 / resolution).toInt()) bins), :1391-1457 (getAverageSignalLevel,
+ * detectSignal: the whole row [0, N-1]) and :1462-1540 (detectSignalsInFFT,
+ * +-2 bins per step); the window arithmetic and thresholds stay with the caller
+ * (rfanalyzer_amd/scanner.py mirrors them).  Synchronous, host arrays. */
+RFA_API int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, size_t count, float *peak,
+                                 float *avg);
 
 /* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers. */
 RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);

@@ -108,6 +108,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_retune_offset": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int, ctypes.c_int64]),
         "rfa_set_channel": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
         "rfa_draw_preprocess": (ctypes.c_int, [_h, ctypes.POINTER(RfaDrawParams), _vp, _fp, _fp, _fp]),
+        "rfa_row_window_stats": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                                ctypes.c_size_t, _fp, _fp]),
         "rfa_get_channel_means": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t,
                                                  ctypes.POINTER(ctypes.c_size_t)]),
     }

@@ -115,6 +115,56 @@ __global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
     }
 }
 
+// Newest-row window statistics for the scanners and squelch (SURVEY.md §8(f)
+// row 2; MainViewModel.kt:861-929 detectIEMChannelsInFFT, :1391-1457
+// getAverageSignalLevel / detectSignal, :1462-1540 detectSignalsInFFT): for every
+// window [lo, hi] (inclusive bins of the fft-shifted row) the peak
+// (FloatArray.maxOrNull: NaN wins) and FloatArray.average() -- a double sum
+// divided by the count, then toFloat().  One workgroup per window; the double
+// partial sums meet in LDS (a different summation order than the JVM's
+// sequential one, equal after the final rounding to float up to one ulp).
+__global__ void __launch_bounds__(256) row_window_kernel(const float *row, const int *lo, const int *hi, int count,
+                                                         float *peak, float *avg) {
+    const int w = blockIdx.x;
+    if (w >= count) return;
+    const int a = lo[w], b = hi[w];
+    float mx = -INFINITY;
+    bool nan = false;
+    double s = 0.0;
+    for (int j = a + (int)threadIdx.x; j <= b; j += 256) {
+        const float x = row[j];
+        nan |= x != x;
+        mx = x > mx ? x : mx;
+        s += (double)x;
+    }
+    __shared__ double ss[256];
+    __shared__ float sm[256];
+    __shared__ int sn[256];
+    ss[threadIdx.x] = s;
+    sm[threadIdx.x] = mx;
+    sn[threadIdx.x] = nan;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            ss[threadIdx.x] += ss[threadIdx.x + k];
+            sm[threadIdx.x] = fmaxf(sm[threadIdx.x], sm[threadIdx.x + k]);
+            sn[threadIdx.x] |= sn[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        peak[w] = sn[0] ? NAN : sm[0];
+        avg[w] = (float)(ss[0] / (double)(b - a + 1));
+    }
+}
+
+hipError_t launch_row_windows(const float *row, const int *lo, const int *hi, int count, float *peak, float *avg,
+                              hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(row_window_kernel, dim3(count), dim3(256), 0, s, row, lo, hi, count, peak, avg);
+    return hipGetLastError();
+}
+
 hipError_t launch_draw(const DrawLaunch &a) {
     if (a.width <= 0 || a.ring_rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(draw_rows_kernel, dim3((a.width + 255) / 256, a.ring_rows), dim3(256), 0, a.stream, a);

@@ -820,6 +820,30 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
     return RFA_OK;
 }
 
+int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, size_t count, float *peak, float *avg) {
+    if (!h || (count && (!lo || !hi || !peak || !avg)) || count > (size_t)0x7fffffff) return RFA_ERR_INVALID;
+    if (!h->d_ring) return fail(h, RFA_ERR_STATE, "window statistics read the newest ring row (ring_rows > 0)");
+    for (size_t i = 0; i < count; i++)
+        if (lo[i] < 0 || hi[i] >= h->n || lo[i] > hi[i]) return fail(h, RFA_ERR_INVALID, "window outside the row");
+    if (count == 0) return RFA_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    const size_t b = (count * 4 + 255) & ~(size_t)255;
+    rc = ensure_device_buffer(h, &h->d_draw, &h->d_draw_cap, 4 * b);
+    if (rc) return rc;
+    char *base = static_cast<char *>(h->d_draw);
+    int *d_lo = reinterpret_cast<int *>(base), *d_hi = reinterpret_cast<int *>(base + b);
+    float *d_pk = reinterpret_cast<float *>(base + 2 * b), *d_av = reinterpret_cast<float *>(base + 3 * b);
+    HIPCHK(h, hipMemcpyAsync(d_lo, lo, count * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(d_hi, hi, count * 4, hipMemcpyHostToDevice, h->stream));
+    const float *row = h->d_ring + (size_t)h->read_index * h->n;  // FftProcessorData.readIndex: newest row
+    HIPCHK(h, rfa::launch_row_windows(row, d_lo, d_hi, (int)count, d_pk, d_av, h->stream));
+    HIPCHK(h, hipMemcpyAsync(peak, d_pk, count * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(avg, d_av, count * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
 int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency) {
     if (!h) return RFA_ERR_INVALID;
     h->chan_on = start_frequency != end_frequency;

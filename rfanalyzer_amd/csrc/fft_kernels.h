@@ -131,6 +131,9 @@ struct DrawLaunch {
     hipStream_t stream = nullptr;
 };
 hipError_t launch_draw(const DrawLaunch &a);
+// Peak / mean of inclusive bin windows of one row (scanner reductions), display.hip.
+hipError_t launch_row_windows(const float *row, const int *lo, const int *hi, int count, float *peak, float *avg,
+                              hipStream_t s);
 
 // Ring maintenance (FftProcessor.kt:197-220) and boxcar (AnalyzerSurface.kt:710-714).
 hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);

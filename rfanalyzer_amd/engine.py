@@ -212,6 +212,20 @@ class SpectrumEngine:
                     "rfa_draw_preprocess")
         return colors, path, pk, (float(mm[0]), float(mm[1]))
 
+    def row_window_stats(self, lo, hi):
+        """(peak, avg) float32 arrays over inclusive bin windows [lo, hi] of the newest ring row
+        (MainViewModel.kt scanner / squelch reductions)."""
+        lo = np.ascontiguousarray(lo, dtype=np.int32)
+        hi = np.ascontiguousarray(hi, dtype=np.int32)
+        if lo.shape != hi.shape:
+            raise ValueError("lo and hi differ in length")
+        pk = np.empty(lo.size, np.float32)
+        av = np.empty(lo.size, np.float32)
+        i32 = ctypes.POINTER(ctypes.c_int32)
+        self._check(_lib.lib().rfa_row_window_stats(self._h, lo.ctypes.data_as(i32), hi.ctypes.data_as(i32), lo.size,
+                                                    _fptr(pk), _fptr(av)), "rfa_row_window_stats")
+        return pk, av
+
     def main_kernel_name(self) -> str:
         """HIP kernel that rfa_process launches for this configuration (rocprofv3 name)."""
         return _lib.lib().rfa_main_kernel_name(self._h).decode()
