@@ -603,7 +603,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                     }
                 }
             };
-            static_assert(!STG || PT == 32, "pending-store wait counts assume 32 stores per destination");
             pending_st = (a.rows ? PT : 0) + (to_ring ? PT : 0);
             if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
             else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
