@@ -23,6 +23,8 @@
  *     ui/AnalyzerSurface.kt:599-743
  *   MainViewModel scanner / squelch row reductions          rfa_row_window_stats()
  *     ui/MainViewModel.kt:861-929,1391-1540
+ *   IQConverter.mixPacketIntoSamplePacket + Decimator      rfa_ddc_*() (demod front end, below)
+ *     source/Signed8BitIQConverter.java:53-131, analyzer/Decimator.java:175-191
  *   (north-star extension) exponential average             rfa_get_ema()
  *     idiom of database/GlobalPerformanceData.kt:44-50
  *
@@ -225,6 +227,63 @@ RFA_API int64_t rfa_retune_offset(int64_t frequency_diff, int n, int64_t sample_
 /* Name of the HIP kernel rfa_process launches for this handle's configuration
  * ("fft_wide_kernel" or "fft_rows_kernel"), as rocprofv3 reports it. */
 RFA_API const char *rfa_main_kernel_name(const rfa_handle *h);
+
+/* ------------------------------------------------------------------------
+ * Demod-branch front end: NCO down-mix of raw IQ
+ * bytes + decimating low-pass FIR, one handle per demodulated channel.
+ * Replaces (app paths as above):
+ *   IQConverter.mixPacketIntoSamplePacket        rfa_ddc_set_frequencies() +
+ *     source/Signed8BitIQConverter.java:53-131,    rfa_ddc_process()
+ *     Unsigned8BitIQConverter.java:53-131,
+ *     Signed16BitIQConverter.kt:59-181, IQConverter.java:64-76
+ *   Decimator.downsampling / FirFilter.filter    rfa_ddc_process()
+ *     analyzer/Decimator.java:175-191, dsp/FirFilter.kt:63-107
+ *   FirFilter.createLowPassTaps                  rfa_lowpass_taps()  (host only)
+ *     dsp/FirFilter.kt:134-195, dsp/WindowFunctions.kt:44-52
+ * The filter state (delay line, decimation counter) and the mixer's cosine
+ * index carry over between calls exactly as in the reference, so one call on
+ * a long buffer equals the reference run packet by packet.
+ * ------------------------------------------------------------------------ */
+typedef struct rfa_ddc rfa_ddc;
+
+/* input_format: RFA_IN_S8 / RFA_IN_U8 / RFA_IN_S16LE are mixed then filtered;
+ * RFA_IN_F32_INTERLEAVED is taken as already-mixed samples and only filtered
+ * (the Decimator on a float SamplePacket).  Decimation = sample_rate /
+ * output_sample_rate; taps = createLowPassTaps(decimation, 1, sample_rate,
+ * 0.75 * out, 0.25 * out, 60) (Decimator.java:177-181).  RFA_ERR_INVALID where
+ * the reference's filter design returns null. */
+RFA_API int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
+                           rfa_ddc **out);
+RFA_API int rfa_ddc_destroy(rfa_ddc *d);
+RFA_API const char *rfa_ddc_last_error(const rfa_ddc *d);
+/* Like IQConverter.setSampleRate + the Decimator's rebuild check: the mixer
+ * table is invalidated; the filter is rebuilt (fresh delay line) only when the
+ * integer decimation changes (Decimator.java:177-178). */
+RFA_API int rfa_ddc_set_sample_rate(rfa_ddc *d, int32_t sample_rate);
+/* mixFrequency = (int)(frequency - channel_frequency), folded by +sample_rate
+ * when 0 or when sample_rate / |mix| > 500; the table (and the cosine index)
+ * is regenerated only when the folded frequency changes. */
+RFA_API int rfa_ddc_set_frequencies(rfa_ddc *d, int64_t frequency, int64_t channel_frequency);
+/* n_samples complex samples of raw input at device address `in` -> the
+ * decimated outputs at device out_re/out_im (planar float).  *n_out is set on
+ * return (computed on the host); RFA_ERR_SIZE if it would exceed out_capacity
+ * (nothing is consumed then).  Asynchronous on the handle's stream. */
+RFA_API int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re, float *out_im,
+                            size_t out_capacity, size_t *n_out);
+/* Same with host buffers; synchronous. */
+RFA_API int rfa_ddc_process_host(rfa_ddc *d, const void *in, size_t n_samples, float *out_re, float *out_im,
+                                 size_t out_capacity, size_t *n_out);
+RFA_API int rfa_ddc_synchronize(rfa_ddc *d);
+RFA_API int rfa_ddc_get_stream(const rfa_ddc *d, void **stream);
+/* Current design: taps (capacity floats), mixer cos/sin per time step
+ * (capacity floats each, may be NULL), counts and folded mix frequency. */
+RFA_API int rfa_ddc_get_taps(const rfa_ddc *d, float *taps, size_t capacity, int32_t *num_taps, int32_t *decimation);
+RFA_API int rfa_ddc_get_mixer(const rfa_ddc *d, float *cos_t, float *sin_t, size_t capacity, int32_t *length,
+                              int32_t *mix_frequency, int32_t *cosine_index);
+/* Host-only filter design, FirFilter.createLowPassTaps with a Blackman window
+ * (no device work).  *num_taps is always set; taps written when it fits. */
+RFA_API int rfa_lowpass_taps(float gain, float sample_rate, float cutoff, float transition, float attenuation,
+                             int32_t max_taps, float *taps, size_t capacity, int32_t *num_taps);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,248 @@
+"""TEST INFRASTRUCTURE ONLY -- restatement of the reference's demod-branch front end.
+
+SURVEY.md §8(f) row 4: the NCO down-mix of raw IQ bytes
+(``IQConverter.mixPacketIntoSamplePacket``) followed by the decimating low-pass
+FIR (``Decimator.downsampling`` -> ``FirFilter.filter``).  Paths relative to
+app/src/main/java/com/mantz_it/rfanalyzer/:
+
+* mixer fold and table: source/Signed8BitIQConverter.java:53-77 (u8 identical,
+  Unsigned8BitIQConverter.java:53-77 with the (i-127.4f)/128 LUT),
+  source/Signed16BitIQConverter.kt:59-87 (different angle rounding);
+* table length: source/IQConverter.java:64-76 (calcOptimalCosineLength);
+* mix loop: Signed8BitIQConverter.java:101-130, Signed16BitIQConverter.kt:126-181;
+* filter design: dsp/FirFilter.kt:134-195 (createLowPassTaps, Blackman window of
+  dsp/WindowFunctions.kt:44-52) with the arguments of analyzer/Decimator.java:177-181;
+* filter loop: dsp/FirFilter.kt:63-107 (circular delay line, decimationCounter
+  starting at 1, sequential float sum newest sample first).
+
+Float32 semantics are kept per operation (numpy float32 scalars and arrays round
+every product and sum; no fused multiply-add).  ``math.sin``/``math.cos`` are the
+platform libm; the JVM's Math.sin/cos may differ from it by one double ulp, which
+after the cast to float almost never shows -- the device library computes its
+tables with the same libm, so GPU parity with this file is exact, and parity with
+the JVM is pinned only through the reference's own test (ResamplerTest.kt:20-116:
+a 100 Hz tone through Decimator 48 kHz -> 12 kHz) as a property, not by vectors.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+F32 = np.float32
+MAX_COSINE_LENGTH = 500                      # IQConverter.java:39
+IN_S8, IN_U8, IN_S16LE, IN_F32_INTERLEAVED = 0, 1, 2, 3
+
+
+def _i32(v: int) -> int:
+    return (v + 2 ** 31) % 2 ** 32 - 2 ** 31
+
+
+def _jtoint(x: float) -> int:
+    """Java/Kotlin (int) of a double: truncate, saturate, NaN -> 0."""
+    if math.isnan(x):
+        return 0
+    if x >= 2 ** 31 - 1:
+        return 2 ** 31 - 1
+    if x <= -2 ** 31:
+        return -2 ** 31
+    return int(x)
+
+
+def mix_frequency(frequency: int, channel_frequency: int, sample_rate: int) -> int:
+    """(int)(frequency - channelFrequency) then the fold of generateMixerLookupTable:
+    += sampleRate when 0 or when sampleRate / |mix| > MAX_COSINE_LENGTH (int math)."""
+    mix = _i32(frequency - channel_frequency)
+    a = abs(mix) if mix != -2 ** 31 else mix          # Math.abs(Integer.MIN_VALUE) stays negative
+    q = (abs(sample_rate) // abs(a)) * (1 if (sample_rate < 0) == (a < 0) else -1) if a != 0 else 0  # truncating
+    if mix == 0 or q > MAX_COSINE_LENGTH:
+        mix = _i32(mix + sample_rate)
+    return mix
+
+
+def optimal_cosine_length(sample_rate: int, cosine_frequency: int) -> int:
+    """IQConverter.calcOptimalCosineLength (IQConverter.java:64-76)."""
+    cycle = sample_rate / abs(float(cosine_frequency))
+    best = _jtoint(cycle)
+    err = abs(best - cycle)
+    i = 1
+    while i * cycle < MAX_COSINE_LENGTH:
+        if abs(i * cycle - _jtoint(i * cycle)) < err:
+            best = _jtoint(i * cycle)
+            err = abs(best - i * cycle)
+        i += 1
+    return best
+
+
+def mixer_table(fmt: int, sample_rate: int, cosine_frequency: int):
+    """Per-time-step cos/sin (float) of the mixer table.  The 8-bit converters store
+    lut[b] * cos_t; that product is formed per sample in ``mix`` with the same rounding."""
+    n = optimal_cosine_length(sample_rate, cosine_frequency)
+    c = np.empty(n, F32)
+    s = np.empty(n, F32)
+    if fmt == IN_S16LE:   # Signed16BitIQConverter.kt:73-81
+        w = (2.0 * math.pi * cosine_frequency) / float(sample_rate)
+        for t in range(n):
+            c[t] = F32(math.cos(w * t))
+            s[t] = F32(math.sin(w * t))
+    else:                 # Signed8BitIQConverter.java:68-70: 2*PI*f*t / (float)sampleRate in double
+        fsr = float(F32(sample_rate))
+        for t in range(n):
+            x = 2 * math.pi * cosine_frequency * t / fsr
+            c[t] = F32(math.cos(x))
+            s[t] = F32(math.sin(x))
+    return c, s
+
+
+def lut(fmt: int, raw: bytes | np.ndarray):
+    """Byte -> float lookup of the three converters: (I, Q) float32 arrays."""
+    raw = np.frombuffer(bytes(raw), np.uint8) if not isinstance(raw, np.ndarray) else raw
+    if fmt == IN_S8:
+        v = raw.view(np.int8).astype(F32) / F32(128.0)
+    elif fmt == IN_U8:
+        v = (raw.astype(F32) - F32(127.4)) / F32(128.0)
+    elif fmt == IN_S16LE:
+        v = raw.view("<i2").astype(F32) / F32(32768.0)
+    else:
+        raise ValueError(fmt)
+    return v[0::2], v[1::2]
+
+
+def mix(fmt: int, raw, cos_t, sin_t, cosine_index: int):
+    """mixPacketIntoSamplePacket body: re = I*c - Q*s, im = Q*c + I*s, index wraps."""
+    i, q = lut(fmt, raw)
+    t = (cosine_index + np.arange(len(i))) % len(cos_t)
+    c, s = cos_t[t], sin_t[t]
+    return (i * c - q * s).astype(F32), (q * c + i * s).astype(F32)
+
+
+def blackman(n: int, N: int) -> np.float32:
+    """BlackmanWindow.value (WindowFunctions.kt:44-49)."""
+    c1 = F32(math.cos(2.0 * math.pi * n / (N - 1)))
+    c2 = F32(math.cos(4.0 * math.pi * n / (N - 1)))
+    return F32(F32(F32(0.42) - F32(0.5) * c1) + F32(0.08) * c2)
+
+
+def low_pass_taps(gain: float, sample_rate: float, cutoff: float, transition: float, attenuation: float,
+                  max_taps: int = 0):
+    """FirFilter.createLowPassTaps (FirFilter.kt:134-195); None where it returns null."""
+    g, fs, fc, tw, att = (F32(v) for v in (gain, sample_rate, cutoff, transition, attenuation))
+    if fs <= 0.0 or fc <= 0.0 or fc > fs / F32(2) or tw <= 0:
+        return None
+    ntaps = _jtoint(float(att * fs) / (22.0 * float(tw)))
+    if max_taps > 0:
+        ntaps = min(ntaps, max_taps)
+    if ntaps & 1 == 0:
+        ntaps += 1
+    pi = F32(math.pi)
+    taps = np.empty(ntaps, F32)
+    M = (ntaps - 1) // 2
+    fwt0 = F32(F32(F32(2) * pi) * fc) / fs
+    for n in range(-M, M + 1):
+        w = blackman(n + M, ntaps)
+        if n == 0:
+            taps[n + M] = F32(fwt0 / pi) * w
+        else:
+            taps[n + M] = F32(F32(math.sin(float(F32(n) * fwt0))) / F32(F32(n) * pi)) * w
+    fmax = taps[M]
+    for n in range(1, M + 1):
+        fmax = F32(fmax + F32(2) * taps[n + M])
+    gain_n = F32(g / fmax)
+    return (taps * gain_n).astype(F32)
+
+
+def decimator_taps(sample_rate: int, output_rate: int):
+    """Decimator.downsampling's filter (Decimator.java:177-181)."""
+    d = int(sample_rate / output_rate)
+    taps = low_pass_taps(1, float(F32(sample_rate)), F32(output_rate) * F32(0.75), F32(output_rate) * F32(0.25), 60)
+    return d, taps
+
+
+class FirDecimator:
+    """FirFilter.filter state machine (FirFilter.kt:42-46,63-107): delay line of
+    len(taps) zeros, tapCounter 0, decimationCounter 1.  ``filter`` is the
+    vectorised form (outputs at once, taps in the reference's order);
+    ``filter_literal`` is the per-sample loop for small cases."""
+
+    def __init__(self, taps, decimation: int):
+        self.taps = np.asarray(taps, F32)
+        self.d = decimation
+        T = len(self.taps)
+        self.hist_re = np.zeros(T - 1, F32)   # the T-1 newest samples before the next input
+        self.hist_im = np.zeros(T - 1, F32)
+        self.counter = 1
+        # literal-form state
+        self._dre = np.zeros(T, F32)
+        self._dim = np.zeros(T, F32)
+        self._tap = 0
+
+    def filter(self, re, im):
+        re, im = np.asarray(re, F32), np.asarray(im, F32)
+        T, S, D = len(self.taps), len(re), self.d
+        xre = np.concatenate([self.hist_re, re])
+        xim = np.concatenate([self.hist_im, im])
+        first = (D - self.counter) % D if D > 0 else 0
+        js = np.arange(first, S, max(D, 1))
+        ore = np.zeros(len(js), F32)
+        oim = np.zeros(len(js), F32)
+        for k in range(T):
+            ore = ore + self.taps[k] * xre[T - 1 + js - k]
+            oim = oim + self.taps[k] * xim[T - 1 + js - k]
+        self.hist_re = xre[len(xre) - (T - 1):].copy() if T > 1 else xre[:0]
+        self.hist_im = xim[len(xim) - (T - 1):].copy() if T > 1 else xim[:0]
+        self.counter = (self.counter + S) % D if D > 0 else 0
+        return ore.astype(F32), oim.astype(F32)
+
+    def filter_literal(self, re, im):
+        taps, T = self.taps, len(self.taps)
+        out_re, out_im = [], []
+        for x, y in zip(np.asarray(re, F32), np.asarray(im, F32)):
+            self._dre[self._tap] = x
+            self._dim[self._tap] = y
+            if self.counter == 0:
+                a, b = F32(0), F32(0)
+                idx = self._tap
+                for t in taps:
+                    a = F32(a + F32(t * self._dre[idx]))
+                    b = F32(b + F32(t * self._dim[idx]))
+                    idx = idx - 1 if idx > 0 else T - 1
+                out_re.append(a)
+                out_im.append(b)
+            self.counter += 1
+            if self.counter >= self.d:
+                self.counter = 0
+            self._tap = self._tap + 1 if self._tap + 1 < T else 0
+        return np.array(out_re, F32), np.array(out_im, F32)
+
+
+class FrontEnd:
+    """Scheduler demod branch + Decimator for one channel: mix the raw packet, then
+    filter-decimate it.  ``fmt`` IN_F32_INTERLEAVED feeds already-mixed float samples
+    straight to the filter (Decimator on a SamplePacket, ResamplerTest.kt:56-62)."""
+
+    def __init__(self, fmt: int, sample_rate: int, output_rate: int):
+        self.fmt, self.sample_rate = fmt, sample_rate
+        self.d, taps = decimator_taps(sample_rate, output_rate)
+        if taps is None:
+            raise ValueError("filter design rejected the rates")
+        self.fir = FirDecimator(taps, self.d)
+        self.cos_freq = None
+        self.cos_t = self.sin_t = None
+        self.cosine_index = 0
+
+    def set_frequencies(self, frequency: int, channel_frequency: int):
+        mf = mix_frequency(frequency, channel_frequency, self.sample_rate)
+        if self.cos_t is None or mf != self.cos_freq:
+            self.cos_freq = mf
+            self.cos_t, self.sin_t = mixer_table(self.fmt, self.sample_rate, mf)
+            self.cosine_index = 0
+
+    def process(self, raw):
+        if self.fmt == IN_F32_INTERLEAVED:
+            v = np.frombuffer(bytes(raw), F32) if not isinstance(raw, np.ndarray) else raw.view(F32)
+            return self.fir.filter(v[0::2], v[1::2])
+        if len(self.cos_t) == 0:
+            return np.zeros(0, F32), np.zeros(0, F32)
+        re, im = mix(self.fmt, raw, self.cos_t, self.sin_t, self.cosine_index)
+        self.cosine_index = (self.cosine_index + len(re)) % len(self.cos_t)
+        return self.fir.filter(re, im)

@@ -112,6 +112,26 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                 ctypes.c_size_t, _fp, _fp]),
         "rfa_get_channel_means": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_float), ctypes.c_size_t,
                                                  ctypes.POINTER(ctypes.c_size_t)]),
+        # demod front end (rfanalyzer_amd/demod.py)
+        "rfa_ddc_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.POINTER(_h)]),
+        "rfa_ddc_destroy": (ctypes.c_int, [_h]),
+        "rfa_ddc_last_error": (ctypes.c_char_p, [_h]),
+        "rfa_ddc_set_sample_rate": (ctypes.c_int, [_h, ctypes.c_int32]),
+        "rfa_ddc_set_frequencies": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
+        "rfa_ddc_process": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_size_t)]),
+        "rfa_ddc_process_host": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, _vp, _vp, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_size_t)]),
+        "rfa_ddc_synchronize": (ctypes.c_int, [_h]),
+        "rfa_ddc_get_stream": (ctypes.c_int, [_h, ctypes.POINTER(_vp)]),
+        "rfa_ddc_get_taps": (ctypes.c_int, [_h, _fp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                            ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_ddc_get_mixer": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int32),
+                                             ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_lowpass_taps": (ctypes.c_int, [ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_int32, _fp, ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_int32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1,0 +1,556 @@
+// ddc.hip -- demod-branch front end on gfx950.
+//
+// One fused kernel per call: every workgroup owns P consecutive decimated
+// outputs, stages the raw IQ bytes they depend on through LDS -- converted and
+// NCO-mixed on the way in (IQConverter.mixPacketIntoSamplePacket,
+// source/Signed8BitIQConverter.java:101-130, Signed16BitIQConverter.kt:126-181)
+// -- and each lane then runs the FIR dot product of one output
+// (FirFilter.filter, dsp/FirFilter.kt:63-107) over LDS.  Raw bytes are read from
+// HBM once plus a halo of T-1 samples per workgroup; only the decimated outputs
+// are written.  The T-1 newest mixed samples of every call are kept on the
+// device as the next call's history (the reference's circular delay line).
+//
+// Bit-exactness: products and sums are separate float roundings in the
+// reference's order (no FMA contraction, taps summed k = 0..T-1, newest sample
+// first), the mixer's lut(b) * cos_t product is the value the reference stores
+// in its table, and the host design code below follows the JVM's float/double
+// promotions step by step.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/rfa.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kCap = 8192;              // staged samples per chunk: re + im = 64 KB LDS
+constexpr int kMaxCosineLength = 500;   // IQConverter.java:39
+
+struct DdcLaunch {
+    const void *raw;
+    long long S;                   // input samples this call
+    const float *hist;             // [re T-1 | im T-1], oldest first, precedes raw[0]
+    float *new_hist;
+    const float *taps;
+    int T;
+    const float *cosv, *sinv;
+    int L, ci;                     // mixer table length, cosine index of raw[0]
+    int D;
+    long long first, n_out;        // first output fires at input `first`
+    int P, KC;                     // outputs per workgroup, taps per LDS chunk
+    float *out_re, *out_im;
+};
+
+template <int FMT>
+__device__ __forceinline__ void ddc_sample(const DdcLaunch &a, long long g, int t, float &re, float &im) {
+    if (g < 0) {
+        re = a.hist[a.T - 1 + g];
+        im = a.hist[2 * (a.T - 1) + g];
+        return;
+    }
+    if constexpr (FMT == RFA_IN_F32_INTERLEAVED) {
+        const float2 v = static_cast<const float2 *>(a.raw)[g];
+        re = v.x;
+        im = v.y;
+        return;
+    } else {
+        float i, q;
+        if constexpr (FMT == RFA_IN_S16LE) {
+            const unsigned v = static_cast<const unsigned *>(a.raw)[g];
+            i = (float)(short)(v & 0xffffu) / 32768.0f;
+            q = (float)(short)(v >> 16) / 32768.0f;
+        } else {
+            const unsigned v = static_cast<const unsigned short *>(a.raw)[g];
+            if constexpr (FMT == RFA_IN_S8) {
+                i = (float)(signed char)(v & 0xffu) / 128.0f;
+                q = (float)(signed char)(v >> 8) / 128.0f;
+            } else {
+                i = ((float)(v & 0xffu) - 127.4f) / 128.0f;
+                q = ((float)(v >> 8) - 127.4f) / 128.0f;
+            }
+        }
+        const float c = a.cosv[t], s = a.sinv[t];
+        re = i * c - q * s;
+        im = q * c + i * s;
+    }
+}
+
+// Table index (cosineIndex) of extended-sequence sample g, for any g.
+__device__ __forceinline__ int cos_index(const DdcLaunch &a, long long g) {
+    if (a.L <= 0) return 0;
+    const long long r = ((long long)a.ci + g) % a.L;
+    return (int)(r < 0 ? r + a.L : r);
+}
+
+template <int FMT>
+__global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
+    __shared__ float sre[kCap];
+    __shared__ float sim[kCap];
+    const int tid = threadIdx.x;
+    const long long m0 = (long long)blockIdx.x * a.P;
+    const int nloc = (int)min((long long)a.P, a.n_out - m0);
+    const long long jb = a.first + m0 * a.D;               // input index of output m0
+    const bool valid = tid < nloc;
+    const int step = a.L > 0 ? kThreads % a.L : 0;
+    float acc_re = 0.0f, acc_im = 0.0f;
+    for (int k0 = 0; k0 < a.T; k0 += a.KC) {
+        const int k1 = min(a.T, k0 + a.KC);
+        const long long lo = jb - (k1 - 1);                 // oldest sample any lane needs
+        const int span = (nloc - 1) * a.D + (k1 - k0);      // <= kCap by the host's choice of P, KC
+        int t = cos_index(a, lo + tid);
+        for (int i = tid; i < span; i += kThreads) {
+            float re, im;
+            ddc_sample<FMT>(a, lo + i, t, re, im);
+            sre[i] = re;
+            sim[i] = im;
+            t += step;
+            if (t >= a.L) t -= a.L;
+        }
+        __syncthreads();
+        if (valid) {
+            const int base = (int)(jb + (long long)tid * a.D - lo);
+            for (int k = k0; k < k1; k++) {
+                const float w = a.taps[k];
+                acc_re = acc_re + w * sre[base - k];
+                acc_im = acc_im + w * sim[base - k];
+            }
+        }
+        __syncthreads();
+    }
+    if (valid) {
+        a.out_re[m0 + tid] = acc_re;
+        a.out_im[m0 + tid] = acc_im;
+    }
+}
+
+// new_hist[t] = sample S - (T-1) + t of the extended sequence [hist | raw].
+template <int FMT>
+__global__ __launch_bounds__(kThreads) void ddc_hist_kernel(DdcLaunch a) {
+    const int t = blockIdx.x * kThreads + threadIdx.x;
+    if (t >= a.T - 1) return;
+    const long long g = a.S - (a.T - 1) + t;
+    float re, im;
+    ddc_sample<FMT>(a, g, cos_index(a, g), re, im);
+    a.new_hist[t] = re;
+    a.new_hist[a.T - 1 + t] = im;
+}
+
+template <int FMT>
+hipError_t launch_ddc(const DdcLaunch &a, hipStream_t st) {
+    if (a.n_out > 0) {
+        const long long blocks = (a.n_out + a.P - 1) / a.P;
+        hipLaunchKernelGGL(ddc_fir_kernel<FMT>, dim3((unsigned)blocks), dim3(kThreads), 0, st, a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (a.T > 1) {
+        hipLaunchKernelGGL(ddc_hist_kernel<FMT>, dim3((a.T - 1 + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a);
+        return hipGetLastError();
+    }
+    return hipSuccess;
+}
+
+// ---------------------------------------------------------------- host design
+
+// Java/Kotlin (int) of a double: truncation, saturation, NaN -> 0.
+int32_t jtoint(double x) {
+    if (x != x) return 0;
+    if (x >= 2147483647.0) return INT32_MAX;
+    if (x <= -2147483648.0) return INT32_MIN;
+    return (int32_t)x;
+}
+
+// BlackmanWindow.value (WindowFunctions.kt:44-49).
+float blackman(int n, int N) {
+    const float c1 = (float)std::cos(2.0 * M_PI * n / (N - 1));
+    const float c2 = (float)std::cos(4.0 * M_PI * n / (N - 1));
+    return 0.42f - 0.5f * c1 + 0.08f * c2;
+}
+
+// FirFilter.createLowPassTaps (FirFilter.kt:134-195).  false where it returns null.
+bool design_low_pass(float gain, float fs, float fc, float tw, float att, int max_taps, std::vector<float> &taps) {
+    if (fs <= 0.0f || fc <= 0.0f || fc > fs / 2 || tw <= 0.0f) return false;
+    int ntaps = jtoint((double)(att * fs) / (22.0 * (double)tw));
+    if (max_taps > 0) ntaps = std::min(ntaps, max_taps);
+    if ((ntaps & 1) == 0) ntaps++;
+    if (ntaps <= 0 || ntaps > (1 << 24)) return false;
+    taps.assign(ntaps, 0.0f);
+    const float pi = (float)M_PI;
+    const int M = (ntaps - 1) / 2;
+    const float fwT0 = 2 * pi * fc / fs;
+    for (int n = -M; n <= M; n++) {
+        const float w = blackman(n + M, ntaps);
+        if (n == 0) taps[n + M] = fwT0 / pi * w;
+        else taps[n + M] = (float)std::sin((double)((float)n * fwT0)) / ((float)n * pi) * w;
+    }
+    float fmx = taps[M];
+    for (int n = 1; n <= M; n++) fmx += 2 * taps[n + M];
+    const float g = gain / fmx;
+    for (float &t : taps) t *= g;
+    return true;
+}
+
+// (int)(frequency - channelFrequency) and the fold of generateMixerLookupTable
+// (Signed8BitIQConverter.java:55-57, Signed16BitIQConverter.kt:62-64).
+int32_t fold_mix(int64_t frequency, int64_t channel, int32_t sr) {
+    int32_t mix = (int32_t)(uint32_t)((uint64_t)frequency - (uint64_t)channel);
+    const int32_t a = mix == INT32_MIN ? INT32_MIN : (mix < 0 ? -mix : mix);
+    const int32_t q = a != 0 ? sr / a : 0;
+    if (mix == 0 || q > kMaxCosineLength) mix = (int32_t)((uint32_t)mix + (uint32_t)sr);
+    return mix;
+}
+
+// IQConverter.calcOptimalCosineLength (IQConverter.java:64-76).
+int optimal_cosine_length(int32_t sr, int32_t cf) {
+    const double cycle = (double)sr / std::fabs((double)cf);
+    int best = jtoint(cycle);
+    double err = std::fabs(best - cycle);
+    for (int i = 1; i * cycle < kMaxCosineLength; i++) {
+        const double ic = i * cycle;
+        if (std::fabs(ic - jtoint(ic)) < err) {
+            best = jtoint(ic);
+            err = std::fabs(best - ic);
+        }
+    }
+    return best;
+}
+
+void mixer_table(int fmt, int32_t sr, int32_t cf, std::vector<float> &c, std::vector<float> &s) {
+    const int n = std::max(0, optimal_cosine_length(sr, cf));
+    c.assign(n, 0.0f);
+    s.assign(n, 0.0f);
+    if (fmt == RFA_IN_S16LE) {  // Signed16BitIQConverter.kt:73-81
+        const double w = (2.0 * M_PI * cf) / (double)sr;
+        for (int t = 0; t < n; t++) {
+            c[t] = (float)std::cos(w * t);
+            s[t] = (float)std::sin(w * t);
+        }
+    } else {                    // Signed8BitIQConverter.java:68-70
+        for (int t = 0; t < n; t++) {
+            const double x = 2 * M_PI * cf * t / (double)(float)sr;
+            c[t] = (float)std::cos(x);
+            s[t] = (float)std::sin(x);
+        }
+    }
+}
+
+}  // namespace
+
+struct rfa_ddc {
+    int device = 0;
+    int fmt = 0;
+    int32_t sample_rate = 0, out_rate = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // mixer (IQConverter state)
+    bool mixer_valid = false;
+    int32_t cos_freq = 0;
+    int ci = 0;
+    std::vector<float> cos_t, sin_t;
+    float *d_cos = nullptr;   // [cos 512 | sin 512]
+    // filter (FirFilter state)
+    int D = 0;
+    std::vector<float> taps;
+    float *d_taps = nullptr;
+    size_t taps_cap = 0;
+    long long dc = 1;         // decimationCounter (FirFilter.kt:46)
+    float *d_hist[2] = {nullptr, nullptr};
+    int cur = 0;
+    // staging for the _host entry point
+    void *d_in = nullptr;
+    size_t d_in_cap = 0;
+    float *d_out = nullptr;
+    size_t d_out_cap = 0;
+};
+
+namespace {
+
+int dfail(rfa_ddc *d, int code, const std::string &msg) {
+    if (d) d->err = msg;
+    return code;
+}
+
+#define DHIP(d, expr)                                                                  \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess) return dfail((d), RFA_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+size_t ddc_sample_bytes(int fmt) {
+    switch (fmt) {
+    case RFA_IN_S8:
+    case RFA_IN_U8: return 2;
+    case RFA_IN_S16LE: return 4;
+    case RFA_IN_F32_INTERLEAVED: return 8;
+    default: return 0;
+    }
+}
+
+// (Re)build the filter for the current rates: new taps, zeroed delay line,
+// decimationCounter 1 (Decimator.java:177-181, FirFilter.kt:42-46).
+int rebuild_filter(rfa_ddc *d) {
+    std::vector<float> taps;
+    const int D = d->sample_rate / d->out_rate;
+    if (!design_low_pass(1.0f, (float)d->sample_rate, d->out_rate * 0.75f, d->out_rate * 0.25f, 60.0f, 0, taps))
+        return dfail(d, RFA_ERR_INVALID, "low-pass design rejected the rates (createLowPassTaps returns null)");
+    if (D < 1) return dfail(d, RFA_ERR_INVALID, "output rate above input rate");
+    const size_t T = taps.size();
+    if (T > d->taps_cap) {
+        if (d->d_taps) hipFree(d->d_taps);
+        for (float *&h : d->d_hist)
+            if (h) hipFree(h), h = nullptr;
+        d->d_taps = nullptr;
+        d->taps_cap = 0;
+        if (hipMalloc(&d->d_taps, T * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc taps");
+        for (float *&h : d->d_hist)
+            if (hipMalloc(&h, 2 * T * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc history");
+        d->taps_cap = T;
+    }
+    DHIP(d, hipMemcpyAsync(d->d_taps, taps.data(), T * sizeof(float), hipMemcpyHostToDevice, d->stream));
+    DHIP(d, hipMemsetAsync(d->d_hist[0], 0, 2 * T * sizeof(float), d->stream));
+    DHIP(d, hipStreamSynchronize(d->stream));
+    d->taps = std::move(taps);
+    d->D = D;
+    d->dc = 1;
+    d->cur = 0;
+    return RFA_OK;
+}
+
+template <int FMT>
+hipError_t dispatch(const DdcLaunch &a, hipStream_t st) {
+    return launch_ddc<FMT>(a, st);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rfa_lowpass_taps(float gain, float sample_rate, float cutoff, float transition, float attenuation,
+                     int32_t max_taps, float *taps, size_t capacity, int32_t *num_taps) {
+    if (!num_taps) return RFA_ERR_INVALID;
+    std::vector<float> t;
+    *num_taps = 0;
+    if (!design_low_pass(gain, sample_rate, cutoff, transition, attenuation, max_taps, t)) return RFA_ERR_INVALID;
+    *num_taps = (int32_t)t.size();
+    if (taps) {
+        if (capacity < t.size()) return RFA_ERR_SIZE;
+        std::memcpy(taps, t.data(), t.size() * sizeof(float));
+    }
+    return RFA_OK;
+}
+
+int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate, rfa_ddc **out) {
+    if (!out) return RFA_ERR_INVALID;
+    *out = nullptr;
+    if (ddc_sample_bytes(input_format) == 0 || sample_rate <= 0 || output_sample_rate <= 0) return RFA_ERR_INVALID;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return RFA_ERR_NODEVICE;
+    if (device < 0 || device >= count) return RFA_ERR_INVALID;
+    rfa_ddc *d = new (std::nothrow) rfa_ddc();
+    if (!d) return RFA_ERR_NOMEM;
+    d->device = device;
+    d->fmt = input_format;
+    d->sample_rate = sample_rate;
+    d->out_rate = output_sample_rate;
+    int rc = RFA_OK;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess)
+        rc = RFA_ERR_HIP;
+    else if (hipMalloc(&d->d_cos, 2 * 512 * sizeof(float)) != hipSuccess)
+        rc = RFA_ERR_NOMEM;
+    else
+        rc = rebuild_filter(d);
+    if (rc != RFA_OK) {
+        rfa_ddc_destroy(d);
+        return rc;
+    }
+    *out = d;
+    return RFA_OK;
+}
+
+int rfa_ddc_destroy(rfa_ddc *d) {
+    if (!d) return RFA_ERR_INVALID;
+    hipSetDevice(d->device);
+    if (d->stream) hipStreamSynchronize(d->stream);
+    for (void *p : {(void *)d->d_cos, (void *)d->d_taps, (void *)d->d_hist[0], (void *)d->d_hist[1], d->d_in,
+                    (void *)d->d_out})
+        if (p) hipFree(p);
+    if (d->stream) hipStreamDestroy(d->stream);
+    delete d;
+    return RFA_OK;
+}
+
+const char *rfa_ddc_last_error(const rfa_ddc *d) { return d ? d->err.c_str() : "null handle"; }
+
+int rfa_ddc_set_sample_rate(rfa_ddc *d, int32_t sample_rate) {
+    if (!d || sample_rate <= 0) return RFA_ERR_INVALID;
+    if (sample_rate == d->sample_rate) return RFA_OK;
+    DHIP(d, hipSetDevice(d->device));
+    const int32_t old = d->sample_rate;
+    d->sample_rate = sample_rate;
+    d->mixer_valid = false;                      // IQConverter.setSampleRate: cosineFrequency = -1
+    if (sample_rate / d->out_rate != d->D) {
+        const int rc = rebuild_filter(d);
+        if (rc != RFA_OK) {
+            d->sample_rate = old;
+            return rc;
+        }
+    }
+    return RFA_OK;
+}
+
+int rfa_ddc_set_frequencies(rfa_ddc *d, int64_t frequency, int64_t channel_frequency) {
+    if (!d) return RFA_ERR_INVALID;
+    if (d->fmt == RFA_IN_F32_INTERLEAVED) return RFA_OK;  // samples arrive mixed
+    const int32_t mf = fold_mix(frequency, channel_frequency, d->sample_rate);
+    if (d->mixer_valid && mf == d->cos_freq) return RFA_OK;
+    std::vector<float> c, s;
+    mixer_table(d->fmt, d->sample_rate, mf, c, s);
+    if (c.size() > 512) return dfail(d, RFA_ERR_UNSUPPORTED, "mixer table longer than 512");
+    DHIP(d, hipSetDevice(d->device));
+    if (!c.empty()) {
+        DHIP(d, hipMemcpyAsync(d->d_cos, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice, d->stream));
+        DHIP(d, hipMemcpyAsync(d->d_cos + 512, s.data(), s.size() * sizeof(float), hipMemcpyHostToDevice, d->stream));
+        DHIP(d, hipStreamSynchronize(d->stream));
+    }
+    d->cos_t = std::move(c);
+    d->sin_t = std::move(s);
+    d->cos_freq = mf;
+    d->ci = 0;
+    d->mixer_valid = true;
+    return RFA_OK;
+}
+
+int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re, float *out_im, size_t out_capacity,
+                    size_t *n_out) {
+    if (!d || !n_out) return RFA_ERR_INVALID;
+    *n_out = 0;
+    if (n_samples == 0) return RFA_OK;
+    const size_t sb = ddc_sample_bytes(d->fmt);
+    if (!in || (uintptr_t)in % std::min<size_t>(sb, 8) != 0) return dfail(d, RFA_ERR_INVALID, "input pointer null or misaligned");
+    if (n_samples > (size_t)1 << 40) return dfail(d, RFA_ERR_INVALID, "n_samples too large");
+    const bool mixed = d->fmt != RFA_IN_F32_INTERLEAVED;
+    if (mixed && !d->mixer_valid) return dfail(d, RFA_ERR_STATE, "rfa_ddc_set_frequencies not called");
+    if (mixed && d->cos_t.empty()) return RFA_OK;   // empty table: the reference mixes nothing
+    const long long S = (long long)n_samples, D = d->D;
+    const long long first = (D - d->dc % D) % D;
+    const long long n = first < S ? (S - 1 - first) / D + 1 : 0;
+    if ((size_t)n > out_capacity) return dfail(d, RFA_ERR_SIZE, "output capacity too small");
+    if (n > 0 && (!out_re || !out_im)) return RFA_ERR_INVALID;
+    DHIP(d, hipSetDevice(d->device));
+    DdcLaunch a{};
+    a.raw = in;
+    a.S = S;
+    a.hist = d->d_hist[d->cur];
+    a.new_hist = d->d_hist[d->cur ^ 1];
+    a.taps = d->d_taps;
+    a.T = (int)d->taps.size();
+    a.cosv = d->d_cos;
+    a.sinv = d->d_cos + 512;
+    a.L = mixed ? (int)d->cos_t.size() : 0;
+    a.ci = d->ci;
+    a.D = (int)D;
+    a.first = first;
+    a.n_out = n;
+    a.P = (int)std::min<long long>(kThreads, std::max<long long>(1, (kCap / 2) / D));
+    a.KC = kCap - (a.P - 1) * a.D;
+    a.out_re = out_re;
+    a.out_im = out_im;
+    hipError_t e = hipSuccess;
+    switch (d->fmt) {
+    case RFA_IN_S8: e = dispatch<RFA_IN_S8>(a, d->stream); break;
+    case RFA_IN_U8: e = dispatch<RFA_IN_U8>(a, d->stream); break;
+    case RFA_IN_S16LE: e = dispatch<RFA_IN_S16LE>(a, d->stream); break;
+    default: e = dispatch<RFA_IN_F32_INTERLEAVED>(a, d->stream); break;
+    }
+    if (e != hipSuccess) return dfail(d, RFA_ERR_HIP, std::string("ddc launch: ") + hipGetErrorString(e));
+    if (a.T > 1) d->cur ^= 1;
+    d->dc = (d->dc + S) % D;
+    if (mixed) d->ci = (int)(((long long)d->ci + S) % (long long)d->cos_t.size());
+    *n_out = (size_t)n;
+    return RFA_OK;
+}
+
+int rfa_ddc_process_host(rfa_ddc *d, const void *in, size_t n_samples, float *out_re, float *out_im,
+                         size_t out_capacity, size_t *n_out) {
+    if (!d || !n_out || (n_samples && !in)) return RFA_ERR_INVALID;
+    *n_out = 0;
+    if (n_samples == 0) return RFA_OK;
+    DHIP(d, hipSetDevice(d->device));
+    const size_t bytes = n_samples * ddc_sample_bytes(d->fmt);
+    const size_t D = (size_t)d->D, most = n_samples / D + 1;
+    if (bytes > d->d_in_cap) {
+        if (d->d_in) hipFree(d->d_in);
+        d->d_in = nullptr;
+        d->d_in_cap = 0;
+        if (hipMalloc(&d->d_in, bytes) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc input staging");
+        d->d_in_cap = bytes;
+    }
+    if (2 * most > d->d_out_cap) {
+        if (d->d_out) hipFree(d->d_out);
+        d->d_out = nullptr;
+        d->d_out_cap = 0;
+        if (hipMalloc(&d->d_out, 2 * most * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc output staging");
+        d->d_out_cap = 2 * most;
+    }
+    DHIP(d, hipMemcpyAsync(d->d_in, in, bytes, hipMemcpyHostToDevice, d->stream));
+    size_t n = 0;
+    const int rc = rfa_ddc_process(d, d->d_in, n_samples, d->d_out, d->d_out + most, out_capacity, &n);
+    if (rc != RFA_OK) return rc;
+    if (n) {
+        DHIP(d, hipMemcpyAsync(out_re, d->d_out, n * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+        DHIP(d, hipMemcpyAsync(out_im, d->d_out + most, n * sizeof(float), hipMemcpyDeviceToHost, d->stream));
+    }
+    DHIP(d, hipStreamSynchronize(d->stream));
+    *n_out = n;
+    return RFA_OK;
+}
+
+int rfa_ddc_synchronize(rfa_ddc *d) {
+    if (!d) return RFA_ERR_INVALID;
+    DHIP(d, hipSetDevice(d->device));
+    DHIP(d, hipStreamSynchronize(d->stream));
+    return RFA_OK;
+}
+
+int rfa_ddc_get_stream(const rfa_ddc *d, void **stream) {
+    if (!d || !stream) return RFA_ERR_INVALID;
+    *stream = (void *)d->stream;
+    return RFA_OK;
+}
+
+int rfa_ddc_get_taps(const rfa_ddc *d, float *taps, size_t capacity, int32_t *num_taps, int32_t *decimation) {
+    if (!d) return RFA_ERR_INVALID;
+    if (num_taps) *num_taps = (int32_t)d->taps.size();
+    if (decimation) *decimation = d->D;
+    if (taps) {
+        if (capacity < d->taps.size()) return RFA_ERR_SIZE;
+        std::memcpy(taps, d->taps.data(), d->taps.size() * sizeof(float));
+    }
+    return RFA_OK;
+}
+
+int rfa_ddc_get_mixer(const rfa_ddc *d, float *cos_t, float *sin_t, size_t capacity, int32_t *length,
+                      int32_t *mix_frequency, int32_t *cosine_index) {
+    if (!d) return RFA_ERR_INVALID;
+    if (d->fmt != RFA_IN_F32_INTERLEAVED && !d->mixer_valid) return RFA_ERR_STATE;
+    if (length) *length = (int32_t)d->cos_t.size();
+    if (mix_frequency) *mix_frequency = d->cos_freq;
+    if (cosine_index) *cosine_index = d->ci;
+    if (cos_t || sin_t) {
+        if (capacity < d->cos_t.size()) return RFA_ERR_SIZE;
+        if (cos_t) std::memcpy(cos_t, d->cos_t.data(), d->cos_t.size() * sizeof(float));
+        if (sin_t) std::memcpy(sin_t, d->sin_t.data(), d->sin_t.size() * sizeof(float));
+    }
+    return RFA_OK;
+}
+
+}  // extern "C"

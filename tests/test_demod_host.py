@@ -1,0 +1,116 @@
+"""CPU: demod front end restatement (oracle/demod.py) and the library's host-side
+filter design (rfa_lowpass_taps).
+
+Parity with the JVM is not pinned by vectors (the reference holds none for this
+branch); it is pinned through the restated per-sample loop of FirFilter.filter
+and the property its own test checks (ResamplerTest.kt:20-116: a 100 Hz tone
+through Decimator 48 kHz -> 12 kHz)."""
+import numpy as np
+import pytest
+
+from oracle import demod as od
+
+F32 = np.float32
+
+
+def test_vectorised_filter_equals_literal_loop_across_packets():
+    rng = np.random.default_rng(5)
+    d, taps = od.decimator_taps(240_000, 24_000)            # D = 10
+    assert d == 10 and len(taps) % 2 == 1
+    a, b = od.FirDecimator(taps, d), od.FirDecimator(taps, d)
+    x = rng.standard_normal((2, 3000)).astype(F32)
+    got_re, got_im, lit_re, lit_im = [], [], [], []
+    pos = 0
+    for n in [1, 7, 0, 130, 999, 3, 1860]:                 # ragged packets, some shorter than the filter
+        r, i = a.filter(x[0, pos:pos + n], x[1, pos:pos + n])
+        lr, li = b.filter_literal(x[0, pos:pos + n], x[1, pos:pos + n])
+        got_re.append(r), got_im.append(i), lit_re.append(lr), lit_im.append(li)
+        pos += n
+    assert pos == 3000
+    np.testing.assert_array_equal(np.concatenate(got_re), np.concatenate(lit_re))
+    np.testing.assert_array_equal(np.concatenate(got_im), np.concatenate(lit_im))
+    assert len(np.concatenate(got_re)) == 300                # outputs at inputs 9, 19, ... (counter starts at 1)
+
+
+def test_decimator_taps_shape_and_gain():
+    d, taps = od.decimator_taps(48_000, 12_000)
+    assert d == 4
+    assert len(taps) == 43                                   # (60*48000/(22*3000)).toInt() = 43, odd
+    assert abs(float(taps.astype(np.float64).sum()) - 1.0) < 1e-5
+    np.testing.assert_array_equal(taps, taps[::-1])          # symmetric
+    assert od.low_pass_taps(1, 48_000, 30_000, 1000, 60) is None   # cutoff above fs/2 -> null
+
+
+def test_resampler_test_tone_passes_the_decimator():
+    """ResamplerTest.kt:20-116 drives Decimator(12000) with a 100 Hz IQ tone at 48 kHz."""
+    n = 48_000
+    t = np.arange(n) / 48_000.0
+    iq = np.empty(2 * n, F32)
+    iq[0::2] = np.cos(2 * np.pi * 100.0 * t).astype(F32)
+    iq[1::2] = np.sin(2 * np.pi * 100.0 * t).astype(F32)
+    fe = od.FrontEnd(od.IN_F32_INTERLEAVED, 48_000, 12_000)
+    outs = [fe.process(iq[k:k + 2048]) for k in range(0, 2 * n, 2048)]   # 1024-sample packets
+    re = np.concatenate([o[0] for o in outs])
+    im = np.concatenate([o[1] for o in outs])
+    assert len(re) == n // 4
+    z = (re + 1j * im)[100:]                                  # past the filter's transient
+    assert np.abs(np.abs(z) - 1).max() < 2e-3                 # pass-band gain 1
+    ang = np.angle(z[1:] * np.conj(z[:-1]))
+    assert np.allclose(ang, 2 * np.pi * 100 / 12_000, atol=1e-3)
+
+
+def test_mixer_fold_and_cosine_length():
+    sr = 2_400_000
+    assert od.mix_frequency(100_000_000, 100_000_000, sr) == sr          # 0 -> +sampleRate
+    assert od.mix_frequency(100_000_000, 100_001_000, sr) == -1000 + sr  # sr/1000 > 500 -> folded
+    assert od.mix_frequency(100_000_000, 99_900_000, sr) == 100_000
+    assert od.optimal_cosine_length(sr, 100_000) == 24
+    assert od.optimal_cosine_length(sr, sr) == 1
+    n = od.optimal_cosine_length(sr, 7_001)                              # best multiple below 500 samples
+    assert 0 < n < 500
+    assert od.mix_frequency(2 ** 40 + 5, 0, sr) == 5 + sr                # (int) keeps the low 32 bits
+
+
+def test_mix_brings_the_channel_to_dc():
+    sr, f, ch = 1_000_000, 100_000_000, 100_125_000
+    n = 4000
+    k = np.arange(n)
+    tone = np.exp(2j * np.pi * (ch - f) / sr * k) * 0.9
+    raw = np.empty(2 * n, np.int8)
+    raw[0::2] = np.round(tone.real * 127).astype(np.int8)
+    raw[1::2] = np.round(tone.imag * 127).astype(np.int8)
+    mf = od.mix_frequency(f, ch, sr)
+    c, s = od.mixer_table(od.IN_S8, sr, mf)
+    re, im = od.mix(od.IN_S8, raw.view(np.uint8), c, s, 0)
+    z = re + 1j * im
+    assert abs(np.mean(z)) > 0.85                              # energy at DC
+    assert np.std(np.angle(z)) < 0.05
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import rfanalyzer_amd
+    rfanalyzer_amd.build()
+    return rfanalyzer_amd.lib()
+
+
+@pytest.mark.parametrize("args", [
+    (1, 48_000, 9_000, 3_000, 60, 0),
+    (1, 2_400_000, 72_000, 24_000, 60, 0),
+    (1, 20_000_000, 288_000, 96_000, 60, 0),
+    (1, 10_000_000, 36_000, 12_000, 60, 500),                 # maxTaps clamp (RationalResampler's use)
+    (2.5, 1_000_000, 10_000, 777, 40, 0),
+])
+def test_library_taps_bit_exact_with_restatement(lib, args):
+    from rfanalyzer_amd import demod
+    got = demod.create_low_pass_taps(*args)
+    want = od.low_pass_taps(*args)
+    assert got.dtype == np.float32 and got.shape == want.shape
+    np.testing.assert_array_equal(got.view(np.int32), want.view(np.int32))
+
+
+def test_library_taps_null_cases(lib):
+    from rfanalyzer_amd import demod
+    assert demod.create_low_pass_taps(1, 0, 100, 10, 60) is None
+    assert demod.create_low_pass_taps(1, 1000, 600, 10, 60) is None
+    assert demod.create_low_pass_taps(1, 1000, 100, 0, 60) is None

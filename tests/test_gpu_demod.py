@@ -1,0 +1,173 @@
+"""GPU: demod front end (rfa_ddc_*) bit-exact against the
+restatement (oracle/demod.py) -- NCO mix of raw s8/u8/s16 bytes + decimating FIR
+with state carried across ragged packets, retunes and rate changes."""
+import numpy as np
+import pytest
+
+from oracle import demod as od
+from rfanalyzer_amd import _lib
+from rfanalyzer_amd import demod
+
+pytestmark = pytest.mark.gpu
+
+FMT = {"s8": od.IN_S8, "u8": od.IN_U8, "s16": od.IN_S16LE, "f32": od.IN_F32_INTERLEAVED}
+SB = {"s8": 2, "u8": 2, "s16": 4, "f32": 8}
+
+
+def _raw(fmt, n, seed):
+    rng = np.random.default_rng(seed)
+    if fmt == "s16":
+        return rng.integers(-32768, 32768, 2 * n, dtype=np.int16).view(np.uint8)
+    if fmt == "f32":
+        return rng.standard_normal(2 * n).astype(np.float32).view(np.uint8)
+    return rng.integers(0, 256, 2 * n, dtype=np.uint8)
+
+
+def _same(a, b):
+    assert a.shape == b.shape, (a.shape, b.shape)
+    np.testing.assert_array_equal(a.view(np.int32), b.view(np.int32))
+
+
+def _run_both(fmt, sr, out, sizes, seed, freqs=(100_000_000, 100_130_000)):
+    raw = _raw(fmt, sum(sizes), seed)
+    ref = od.FrontEnd(FMT[fmt], sr, out)
+    fe = demod.FrontEnd(fmt, sr, out)
+    ref.set_frequencies(*freqs)
+    fe.set_frequencies(*freqs)
+    pos = 0
+    for n in sizes:
+        chunk = raw[pos * SB[fmt]:(pos + n) * SB[fmt]]
+        r_re, r_im = ref.process(chunk)
+        g_re, g_im = fe.process(chunk)
+        _same(g_re, r_re)
+        _same(g_im, r_im)
+        pos += n
+    return fe, ref
+
+
+@pytest.mark.parametrize("fmt", ["s8", "u8", "s16"])
+@pytest.mark.parametrize("sr,out", [(2_400_000, 96_000), (1_000_000, 48_000), (10_000_000, 384_000)])
+def test_mix_and_decimate_bit_exact(rfa, fmt, sr, out):
+    fe, ref = _run_both(fmt, sr, out, [16384, 7, 1, 0, 5000, 123457], seed=sr + len(fmt))
+    c, s, mf, ci = fe.mixer()
+    _same(c, ref.cos_t)
+    _same(s, ref.sin_t)
+    assert mf == ref.cos_freq and ci == ref.cosine_index
+    _same(fe.taps, ref.fir.taps)
+    fe.close()
+
+
+def test_filter_only_resampler_test_rates(rfa):
+    """ResamplerTest.kt's Decimator case: float IQ at 48 kHz -> 12 kHz in 1024-sample packets."""
+    fe, _ = _run_both("f32", 48_000, 12_000, [1024] * 46 + [896], seed=3)
+    fe.close()
+
+
+def test_long_filter_uses_several_lds_chunks(rfa):
+    # 20 MHz -> 10 kHz: D = 2000, 21 819 taps, longer than one LDS chunk
+    fe, ref = _run_both("s8", 20_000_000, 10_000, [150_000, 80_001], seed=8)
+    assert len(fe.taps) > 8192 and fe.decimation == 2000
+    fe.close()
+
+
+def test_whole_buffer_equals_packets(rfa):
+    raw = _raw("s8", 200_000, 11)
+    a = demod.FrontEnd("s8", 2_400_000, 48_000)
+    b = demod.FrontEnd("s8", 2_400_000, 48_000)
+    for fe in (a, b):
+        fe.set_frequencies(433_000_000, 433_250_000)
+    whole = a.process(raw)
+    parts = [b.process(raw[k:k + 2 * 4096]) for k in range(0, raw.size, 2 * 4096)]
+    _same(whole[0], np.concatenate([p[0] for p in parts]))
+    _same(whole[1], np.concatenate([p[1] for p in parts]))
+    a.close(), b.close()
+
+
+def test_retune_and_rate_change(rfa):
+    raw = _raw("u8", 60_000, 12)
+    ref = od.FrontEnd(od.IN_U8, 2_400_000, 48_000)
+    fe = demod.FrontEnd("u8", 2_400_000, 48_000)
+    steps = [(100_000_000, 100_200_000), (100_000_000, 100_200_000), (100_000_000, 99_700_000),
+             (100_000_000, 100_000_000)]
+    pos = 0
+    for f, ch in steps:                    # an unchanged frequency keeps the cosine index
+        ref.set_frequencies(f, ch)
+        fe.set_frequencies(f, ch)
+        chunk = raw[2 * pos:2 * (pos + 15_000)]
+        r = ref.process(chunk)
+        g = fe.process(chunk)
+        _same(g[0], r[0]), _same(g[1], r[1])
+        pos += 15_000
+    # same decimation after a rate change: filter (and its delay line) kept, mixer regenerated
+    fe.set_sample_rate(2_410_000)
+    assert fe.decimation == 50
+    fe.set_frequencies(100_000_000, 100_200_000)
+    c, _, mf, ci = fe.mixer()
+    assert mf == od.mix_frequency(100_000_000, 100_200_000, 2_410_000) and ci == 0
+    # new decimation: rebuilt from scratch
+    fe.set_sample_rate(1_200_000)
+    assert fe.decimation == 25
+    _, taps = od.decimator_taps(1_200_000, 48_000)
+    _same(fe.taps, taps)
+    fe.close()
+
+
+class _Dev:
+    """Device buffer from the same HIP runtime librfa links (/opt/rocm), via ctypes."""
+    hip = None
+
+    def __init__(self, nbytes):
+        import ctypes
+        if _Dev.hip is None:
+            _Dev.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.ptr = ctypes.c_void_p()
+        assert _Dev.hip.hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(max(nbytes, 4))) == 0
+        self.nbytes = nbytes
+
+    def put(self, a):
+        import ctypes
+        a = np.ascontiguousarray(a)
+        assert _Dev.hip.hipMemcpy(self.ptr, a.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(a.nbytes), 1) == 0
+
+    def get(self, n, dtype=np.float32):
+        import ctypes
+        out = np.empty(n, dtype)
+        assert _Dev.hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), self.ptr, ctypes.c_size_t(out.nbytes), 2) == 0
+        return out
+
+    def free(self):
+        _Dev.hip.hipFree(self.ptr)
+
+
+def test_device_pointers_and_capacity(rfa):
+    raw_h = _raw("s16", 50_000, 4)
+    raw = _Dev(raw_h.nbytes)
+    raw.put(raw_h)
+    fe = demod.FrontEnd("s16", 2_000_000, 50_000)
+    fe.set_frequencies(7_000_000, 7_100_000)
+    cap = fe.max_outputs(50_000)
+    re, im = _Dev(4 * cap), _Dev(4 * cap)
+    with pytest.raises(_lib.RfaError) as e:
+        fe.process_device(raw.ptr.value, 50_000, re.ptr.value, im.ptr.value, 5)
+    assert e.value.status == _lib.RFA_ERR_SIZE          # nothing consumed: the next call starts fresh
+    n = fe.process_device(raw.ptr.value, 50_000, re.ptr.value, im.ptr.value, cap)
+    fe.synchronize()
+    ref = od.FrontEnd(od.IN_S16LE, 2_000_000, 50_000)
+    ref.set_frequencies(7_000_000, 7_100_000)
+    r = ref.process(raw_h)
+    assert n == len(r[0]) == 50_000 // 40
+    _same(re.get(n), r[0])
+    _same(im.get(n), r[1])
+    for b in (raw, re, im):
+        b.free()
+    fe.close()
+
+
+def test_errors(rfa):
+    with pytest.raises(_lib.RfaError):
+        demod.FrontEnd("s8", 48_000, 40_000)            # cutoff 30 kHz > fs/2: createLowPassTaps -> null
+    fe = demod.FrontEnd("s8", 1_000_000, 50_000)
+    with pytest.raises(_lib.RfaError) as e:             # mixing before any channel is set
+        fe.process(b"\x00" * 64)
+    assert e.value.status == _lib.RFA_ERR_STATE
+    fe.close()
