@@ -53,6 +53,9 @@ def orc() -> ctypes.CDLL:
         lib.orc_spectrum_rows.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t,
                                           ctypes.c_size_t, _fp, _fp]
         lib.orc_convert.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, _fp, _fp]
+        lib.orc_ddc_process.restype = ctypes.c_size_t
+        lib.orc_ddc_process.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, _fp, _fp, ctypes.c_int, _fp,
+                                        ctypes.c_int, ctypes.c_int, _fp, _fp, ctypes.POINTER(ctypes.c_int32), _fp, _fp]
         _orc = lib
     return _orc
 

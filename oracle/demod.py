@@ -153,7 +153,7 @@ def low_pass_taps(gain: float, sample_rate: float, cutoff: float, transition: fl
 
 def decimator_taps(sample_rate: int, output_rate: int):
     """Decimator.downsampling's filter (Decimator.java:177-181)."""
-    d = int(sample_rate / output_rate)
+    d = sample_rate // output_rate
     taps = low_pass_taps(1, float(F32(sample_rate)), F32(output_rate) * F32(0.75), F32(output_rate) * F32(0.25), 60)
     return d, taps
 
@@ -246,3 +246,43 @@ class FrontEnd:
         re, im = mix(self.fmt, raw, self.cos_t, self.sin_t, self.cosine_index)
         self.cosine_index = (self.cosine_index + len(re)) % len(self.cos_t)
         return self.fir.filter(re, im)
+
+
+class CFrontEnd(FrontEnd):
+    """The same front end through the literal per-sample C loop (rfa_oracle.c
+    orc_ddc_process): second restatement for the tests, scalar CPU baseline for
+    scripts/ddc_bench.py."""
+
+    def __init__(self, fmt: int, sample_rate: int, output_rate: int):
+        super().__init__(fmt, sample_rate, output_rate)
+        T = len(self.fir.taps)
+        self._dre = np.zeros(T, F32)
+        self._dim = np.zeros(T, F32)
+        self._ctr = np.array([0, 1, 0], np.int32)      # tapCounter, decimationCounter, cosineIndex
+
+    def set_frequencies(self, frequency: int, channel_frequency: int):
+        old = self.cos_freq
+        super().set_frequencies(frequency, channel_frequency)
+        if self.cos_freq != old:
+            self._ctr[2] = 0
+
+    def process(self, raw):
+        import ctypes
+        from . import orc
+        buf = np.ascontiguousarray(np.frombuffer(bytes(raw), np.uint8) if not isinstance(raw, np.ndarray)
+                                   else raw.view(np.uint8).reshape(-1))
+        sb = {IN_S8: 2, IN_U8: 2, IN_S16LE: 4, IN_F32_INTERLEAVED: 8}[self.fmt]
+        n = buf.size // sb
+        mixed = self.fmt != IN_F32_INTERLEAVED
+        if mixed and len(self.cos_t) == 0:
+            return np.zeros(0, F32), np.zeros(0, F32)
+        cap = n // self.d + 1
+        ore = np.empty(cap, F32)
+        oim = np.empty(cap, F32)
+        fp = ctypes.POINTER(ctypes.c_float)
+        ptr = (lambda a: a.ctypes.data_as(fp))
+        k = orc().orc_ddc_process(self.fmt, buf.ctypes.data, n, ptr(self.cos_t) if mixed else None,
+                                  ptr(self.sin_t) if mixed else None, len(self.cos_t) if mixed else 0,
+                                  ptr(self.fir.taps), len(self.fir.taps), self.d, ptr(self._dre), ptr(self._dim),
+                                  self._ctr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr(ore), ptr(oim))
+        return ore[:k], oim[:k]

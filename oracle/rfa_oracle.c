@@ -199,3 +199,69 @@ int orc_spectrum_rows(const void *base, int fmt, size_t n, size_t n_frames, size
     }
     return ORC_OK;
 }
+
+/* ------------------------------------------------- demod front end (§8(f) row 4)
+ *
+ * mixPacketIntoSamplePacket (source/Signed8BitIQConverter.java:101-130: the
+ * table entry lut[b] * cos_t is one float product, formed here per sample with
+ * the same rounding; Unsigned8BitIQConverter.java and Signed16BitIQConverter.kt
+ * :126-181 alike) followed by FirFilter.filter (dsp/FirFilter.kt:63-107):
+ * circular delay line, output when decimationCounter == 0, taps summed in
+ * order newest sample first.  One sample at a time, exactly the reference's
+ * loop; the CPU baseline of the demod leg (1 thread, scalar).
+ * state: dre[T], dim[T] delay lines; counters = {tapCounter, decimationCounter,
+ * cosineIndex}.  cos_t == NULL: input is already-mixed interleaved float.
+ * Returns the number of outputs written. */
+size_t orc_ddc_process(int fmt, const void *raw, size_t n, const float *cos_t, const float *sin_t, int L,
+                       const float *taps, int T, int D, float *dre, float *dim, int32_t *counters,
+                       float *out_re, float *out_im) {
+    int tap = counters[0], dc = counters[1], ci = counters[2];
+    size_t k = 0;
+    const uint8_t *b = (const uint8_t *)raw;
+    for (size_t s = 0; s < n; s++) {
+        float re, im;
+        if (!cos_t) {
+            const float *f = (const float *)raw;
+            re = f[2 * s];
+            im = f[2 * s + 1];
+        } else {
+            float i, q;
+            if (fmt == ORC_IN_S16LE) {
+                i = (float)(int16_t)(b[4 * s] | (b[4 * s + 1] << 8)) / 32768.0f;
+                q = (float)(int16_t)(b[4 * s + 2] | (b[4 * s + 3] << 8)) / 32768.0f;
+            } else if (fmt == ORC_IN_U8) {
+                i = ((float)b[2 * s] - 127.4f) / 128.0f;
+                q = ((float)b[2 * s + 1] - 127.4f) / 128.0f;
+            } else {
+                i = (float)(int8_t)b[2 * s] / 128.0f;
+                q = (float)(int8_t)b[2 * s + 1] / 128.0f;
+            }
+            const float c = cos_t[ci], sn = sin_t[ci];
+            const float ic = i * c, qs = q * sn, qc = q * c, is = i * sn;
+            re = ic - qs;
+            im = qc + is;
+            ci = (ci + 1) % L;
+        }
+        dre[tap] = re;
+        dim[tap] = im;
+        if (dc == 0) {
+            float ar = 0.0f, ai = 0.0f;
+            int idx = tap;
+            for (int t = 0; t < T; t++) {
+                const float pr = taps[t] * dre[idx], pi = taps[t] * dim[idx];
+                ar = ar + pr;
+                ai = ai + pi;
+                if (--idx < 0) idx = T - 1;
+            }
+            out_re[k] = ar;
+            out_im[k] = ai;
+            k++;
+        }
+        if (++dc >= D) dc = 0;
+        if (++tap >= T) tap = 0;
+    }
+    counters[0] = tap;
+    counters[1] = dc;
+    counters[2] = ci;
+    return k;
+}

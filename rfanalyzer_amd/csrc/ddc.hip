@@ -31,8 +31,9 @@
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kCap = 8192;              // staged samples per chunk: re + im = 64 KB LDS
+constexpr int kThreads = 256;           // largest workgroup
+constexpr int kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
+constexpr int kMaxWavesPerCu = 32;
 constexpr int kMaxCosineLength = 500;   // IQConverter.java:39
 
 struct DdcLaunch {
@@ -47,6 +48,7 @@ struct DdcLaunch {
     int D;
     long long first, n_out;        // first output fires at input `first`
     int P, KC;                     // outputs per workgroup, taps per LDS chunk
+    int threads, lds_bytes;        // workgroup size (P rounded up to 64), dynamic LDS
     float *out_re, *out_im;
 };
 
@@ -91,44 +93,51 @@ __device__ __forceinline__ int cos_index(const DdcLaunch &a, long long g) {
     return (int)(r < 0 ? r + a.L : r);
 }
 
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+// One lane per decimated output; blockDim = P rounded up to a wave.  The
+// samples all P outputs need for taps [k0, k1) are one contiguous run of
+// (P-1)*D + (k1-k0) samples, staged (converted + mixed) into LDS as (re, im)
+// pairs; each lane then accumulates its taps in the reference's order with
+// packed fp32 multiply and add (v_pk_mul_f32 / v_pk_add_f32: two separately
+// rounded operations, exactly the JVM's tap * delay then +=).
 template <int FMT>
 __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
-    __shared__ float sre[kCap];
-    __shared__ float sim[kCap];
+    extern __shared__ __attribute__((aligned(16))) v2f xs[];
     const int tid = threadIdx.x;
+    const int nth = blockDim.x;
     const long long m0 = (long long)blockIdx.x * a.P;
     const int nloc = (int)min((long long)a.P, a.n_out - m0);
     const long long jb = a.first + m0 * a.D;               // input index of output m0
     const bool valid = tid < nloc;
-    const int step = a.L > 0 ? kThreads % a.L : 0;
-    float acc_re = 0.0f, acc_im = 0.0f;
+    const int step = a.L > 0 ? nth % a.L : 0;
+    v2f acc = {0.0f, 0.0f};
     for (int k0 = 0; k0 < a.T; k0 += a.KC) {
         const int k1 = min(a.T, k0 + a.KC);
         const long long lo = jb - (k1 - 1);                 // oldest sample any lane needs
-        const int span = (nloc - 1) * a.D + (k1 - k0);      // <= kCap by the host's choice of P, KC
+        const int span = (nloc - 1) * a.D + (k1 - k0);      // fits the LDS the host sized
         int t = cos_index(a, lo + tid);
-        for (int i = tid; i < span; i += kThreads) {
+        for (int i = tid; i < span; i += nth) {
             float re, im;
             ddc_sample<FMT>(a, lo + i, t, re, im);
-            sre[i] = re;
-            sim[i] = im;
+            xs[i] = v2f{re, im};
             t += step;
             if (t >= a.L) t -= a.L;
         }
         __syncthreads();
         if (valid) {
-            const int base = (int)(jb + (long long)tid * a.D - lo);
+            const v2f *x = xs + (int)(jb + (long long)tid * a.D - lo);
+#pragma unroll 8
             for (int k = k0; k < k1; k++) {
                 const float w = a.taps[k];
-                acc_re = acc_re + w * sre[base - k];
-                acc_im = acc_im + w * sim[base - k];
+                acc = acc + w * x[-k];
             }
         }
         __syncthreads();
     }
     if (valid) {
-        a.out_re[m0 + tid] = acc_re;
-        a.out_im[m0 + tid] = acc_im;
+        a.out_re[m0 + tid] = acc.x;
+        a.out_im[m0 + tid] = acc.y;
     }
 }
 
@@ -148,7 +157,14 @@ template <int FMT>
 hipError_t launch_ddc(const DdcLaunch &a, hipStream_t st) {
     if (a.n_out > 0) {
         const long long blocks = (a.n_out + a.P - 1) / a.P;
-        hipLaunchKernelGGL(ddc_fir_kernel<FMT>, dim3((unsigned)blocks), dim3(kThreads), 0, st, a);
+        static bool attr_set = false;
+        if (!attr_set) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(ddc_fir_kernel<FMT>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+            if (e != hipSuccess) return e;
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(ddc_fir_kernel<FMT>, dim3((unsigned)blocks), dim3(a.threads), a.lds_bytes, st, a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -325,6 +341,27 @@ int rebuild_filter(rfa_ddc *d) {
     return RFA_OK;
 }
 
+// Outputs per workgroup: the P whose LDS run (P-1)*D + T samples lets the most
+// output lanes be resident per CU (LDS and wave limits); P = 1 with the taps
+// split into LDS-sized chunks when even one output's window does not fit.
+void plan_tiles(DdcLaunch &a) {
+    const long long cap = kLdsBytes / (long long)sizeof(float2);
+    int best_p = 1, best_lanes = -1;
+    for (int P = 1; P <= kThreads; P++) {
+        const long long span = (long long)(P - 1) * a.D + a.T;
+        if (span > cap) break;
+        const int threads = (P + 63) / 64 * 64;
+        const int by_lds = (int)(kLdsBytes / (span * (long long)sizeof(float2)));
+        const int blocks = std::min(by_lds, kMaxWavesPerCu / (threads / 64));
+        const int lanes = P * blocks;
+        if (lanes >= best_lanes) best_lanes = lanes, best_p = P;
+    }
+    a.P = best_p;
+    a.threads = (best_p + 63) / 64 * 64;
+    a.KC = (int)std::min<long long>(a.T, cap - (long long)(a.P - 1) * a.D);
+    a.lds_bytes = (int)(((long long)(a.P - 1) * a.D + a.KC) * (long long)sizeof(float2));
+}
+
 template <int FMT>
 hipError_t dispatch(const DdcLaunch &a, hipStream_t st) {
     return launch_ddc<FMT>(a, st);
@@ -460,8 +497,7 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     a.D = (int)D;
     a.first = first;
     a.n_out = n;
-    a.P = (int)std::min<long long>(kThreads, std::max<long long>(1, (kCap / 2) / D));
-    a.KC = kCap - (a.P - 1) * a.D;
+    plan_tiles(a);
     a.out_re = out_re;
     a.out_im = out_im;
     hipError_t e = hipSuccess;

@@ -114,3 +114,25 @@ def test_library_taps_null_cases(lib):
     assert demod.create_low_pass_taps(1, 0, 100, 10, 60) is None
     assert demod.create_low_pass_taps(1, 1000, 600, 10, 60) is None
     assert demod.create_low_pass_taps(1, 1000, 100, 0, 60) is None
+
+
+@pytest.mark.parametrize("fmt,sr,out", [(od.IN_S8, 2_400_000, 96_000), (od.IN_U8, 1_000_000, 48_000),
+                                        (od.IN_S16LE, 10_000_000, 384_000), (od.IN_F32_INTERLEAVED, 48_000, 12_000)])
+def test_c_loop_equals_vectorised_restatement(fmt, sr, out):
+    """orc_ddc_process (the reference's per-sample loop in C) == FrontEnd (numpy form)."""
+    rng = np.random.default_rng(sr)
+    sb = {od.IN_S8: 2, od.IN_U8: 2, od.IN_S16LE: 4, od.IN_F32_INTERLEAVED: 8}[fmt]
+    n = 40_000
+    raw = (rng.standard_normal(2 * n).astype(F32).view(np.uint8) if fmt == od.IN_F32_INTERLEAVED
+           else rng.integers(0, 256, n * sb, dtype=np.uint8))
+    a, b = od.FrontEnd(fmt, sr, out), od.CFrontEnd(fmt, sr, out)
+    pos = 0
+    for n_s, ch in [(5, 100_050_000), (9000, 100_050_000), (1, 99_990_000), (30_994, 99_990_000)]:
+        a.set_frequencies(100_000_000, ch)
+        b.set_frequencies(100_000_000, ch)
+        chunk = raw[pos * sb:(pos + n_s) * sb]
+        ra, rb = a.process(chunk), b.process(chunk)
+        np.testing.assert_array_equal(ra[0].view(np.int32), rb[0].view(np.int32))
+        np.testing.assert_array_equal(ra[1].view(np.int32), rb[1].view(np.int32))
+        pos += n_s
+    assert pos == n
