@@ -34,6 +34,8 @@ namespace {
 constexpr int kThreads = 256;           // largest workgroup
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
 constexpr int kMaxWavesPerCu = 32;
+constexpr int kMaxTable = 512;        // mixer table capacity (> MAX_COSINE_LENGTH)
+constexpr int kDynLds = kLdsBytes - kMaxTable * 8;  // staged samples; the table takes the rest
 constexpr int kMaxCosineLength = 500;   // IQConverter.java:39
 
 struct DdcLaunch {
@@ -49,8 +51,44 @@ struct DdcLaunch {
     long long first, n_out;        // first output fires at input `first`
     int P, KC;                     // outputs per workgroup, taps per LDS chunk
     int threads, lds_bytes;        // workgroup size (P rounded up to 64), dynamic LDS
+    int pad;                       // LDS row pitch D + pad is odd
+    int kc_pad;                    // floats reserved for the chunk's taps (multiple of 4)
     float *out_re, *out_im;
 };
+
+template <int FMT> struct RawOf { using type = unsigned; };
+template <> struct RawOf<RFA_IN_F32_INTERLEAVED> { using type = float2; };
+
+// One complex input sample as stored (I,Q bytes / int16 pair / float pair).
+template <int FMT>
+__device__ __forceinline__ typename RawOf<FMT>::type load_raw(const DdcLaunch &a, long long g) {
+    if constexpr (FMT == RFA_IN_F32_INTERLEAVED) return static_cast<const float2 *>(a.raw)[g];
+    else if constexpr (FMT == RFA_IN_S16LE) return static_cast<const unsigned *>(a.raw)[g];
+    else return static_cast<const unsigned short *>(a.raw)[g];
+}
+
+// LUT conversion + NCO mix of one raw sample with the table entry (c, s).
+template <int FMT>
+__device__ __forceinline__ void mix_raw(typename RawOf<FMT>::type v, float c, float s, float &re, float &im) {
+    if constexpr (FMT == RFA_IN_F32_INTERLEAVED) {
+        re = v.x;
+        im = v.y;
+    } else {
+        float i, q;
+        if constexpr (FMT == RFA_IN_S16LE) {
+            i = (float)(short)(v & 0xffffu) / 32768.0f;
+            q = (float)(short)(v >> 16) / 32768.0f;
+        } else if constexpr (FMT == RFA_IN_S8) {
+            i = (float)(signed char)(v & 0xffu) / 128.0f;
+            q = (float)(signed char)(v >> 8) / 128.0f;
+        } else {
+            i = ((float)(v & 0xffu) - 127.4f) / 128.0f;
+            q = ((float)(v >> 8) - 127.4f) / 128.0f;
+        }
+        re = i * c - q * s;
+        im = q * c + i * s;
+    }
+}
 
 template <int FMT>
 __device__ __forceinline__ void ddc_sample(const DdcLaunch &a, long long g, int t, float &re, float &im) {
@@ -59,31 +97,9 @@ __device__ __forceinline__ void ddc_sample(const DdcLaunch &a, long long g, int 
         im = a.hist[2 * (a.T - 1) + g];
         return;
     }
-    if constexpr (FMT == RFA_IN_F32_INTERLEAVED) {
-        const float2 v = static_cast<const float2 *>(a.raw)[g];
-        re = v.x;
-        im = v.y;
-        return;
-    } else {
-        float i, q;
-        if constexpr (FMT == RFA_IN_S16LE) {
-            const unsigned v = static_cast<const unsigned *>(a.raw)[g];
-            i = (float)(short)(v & 0xffffu) / 32768.0f;
-            q = (float)(short)(v >> 16) / 32768.0f;
-        } else {
-            const unsigned v = static_cast<const unsigned short *>(a.raw)[g];
-            if constexpr (FMT == RFA_IN_S8) {
-                i = (float)(signed char)(v & 0xffu) / 128.0f;
-                q = (float)(signed char)(v >> 8) / 128.0f;
-            } else {
-                i = ((float)(v & 0xffu) - 127.4f) / 128.0f;
-                q = ((float)(v >> 8) - 127.4f) / 128.0f;
-            }
-        }
-        const float c = a.cosv[t], s = a.sinv[t];
-        re = i * c - q * s;
-        im = q * c + i * s;
-    }
+    const float c = FMT == RFA_IN_F32_INTERLEAVED ? 0.0f : a.cosv[t];
+    const float s = FMT == RFA_IN_F32_INTERLEAVED ? 0.0f : a.sinv[t];
+    mix_raw<FMT>(load_raw<FMT>(a, g), c, s, re, im);
 }
 
 // Table index (cosineIndex) of extended-sequence sample g, for any g.
@@ -98,39 +114,85 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // One lane per decimated output; blockDim = P rounded up to a wave.  The
 // samples all P outputs need for taps [k0, k1) are one contiguous run of
 // (P-1)*D + (k1-k0) samples, staged (converted + mixed) into LDS as (re, im)
-// pairs; each lane then accumulates its taps in the reference's order with
-// packed fp32 multiply and add (v_pk_mul_f32 / v_pk_add_f32: two separately
-// rounded operations, exactly the JVM's tap * delay then +=).
+// pairs in rows of D samples with a row pitch Dp = D + pad, pad making Dp odd:
+// at a given tap the lanes read samples exactly D apart, so an odd pitch puts
+// the 32 lanes of a half-wave on 32 different bank pairs (an even D would give
+// up to a 32-way conflict).  Each lane accumulates its taps in the reference's
+// order with packed fp32 multiply and add (v_pk_mul_f32 / v_pk_add_f32: two
+// separately rounded operations, exactly the JVM's tap * delay then +=); the
+// tap loop runs in segments that stay inside one row, so the LDS pointer just
+// walks down.
 template <int FMT>
 __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
-    extern __shared__ __attribute__((aligned(16))) v2f xs[];
+    extern __shared__ __attribute__((aligned(16))) v2f dyn[];
+    v2f *xs = dyn + a.kc_pad / 2;                           // [taps of the chunk | staged samples]
+    float *wl = reinterpret_cast<float *>(dyn);
+    __shared__ float2 cs[kMaxTable];                        // mixer table (cos, sin)
     const int tid = threadIdx.x;
     const int nth = blockDim.x;
+    for (int i = tid; i < a.L; i += nth) cs[i] = float2{a.cosv[i], a.sinv[i]};
+    __syncthreads();
+    const int D = a.D, Dp = a.D + a.pad;
     const long long m0 = (long long)blockIdx.x * a.P;
     const int nloc = (int)min((long long)a.P, a.n_out - m0);
-    const long long jb = a.first + m0 * a.D;               // input index of output m0
+    const long long jb = a.first + m0 * D;                 // input index of output m0
     const bool valid = tid < nloc;
     const int step = a.L > 0 ? nth % a.L : 0;
+    const int srow = nth / D, scol = nth % D;
     v2f acc = {0.0f, 0.0f};
     for (int k0 = 0; k0 < a.T; k0 += a.KC) {
         const int k1 = min(a.T, k0 + a.KC);
         const long long lo = jb - (k1 - 1);                 // oldest sample any lane needs
-        const int span = (nloc - 1) * a.D + (k1 - k0);      // fits the LDS the host sized
-        int t = cos_index(a, lo + tid);
-        for (int i = tid; i < span; i += nth) {
+        const int span = (nloc - 1) * D + (k1 - k0);        // fits the LDS the host sized
+        for (int i = tid; i < k1 - k0; i += nth) wl[i] = a.taps[k0 + i];
+        // leading samples older than this call come from the history (first workgroups only)
+        const int nh = (int)min((long long)span, max(0LL, -lo));
+        for (int i = tid; i < nh; i += nth) {
             float re, im;
-            ddc_sample<FMT>(a, lo + i, t, re, im);
-            xs[i] = v2f{re, im};
-            t += step;
-            if (t >= a.L) t -= a.L;
+            ddc_sample<FMT>(a, lo + i, 0, re, im);
+            xs[(i / D) * Dp + i % D] = v2f{re, im};
+        }
+        // raw part: U loads in flight per lane before any is converted
+        constexpr int U = 8;
+        const int i0 = nh + tid;
+        int t = cos_index(a, lo + i0);
+        int row = i0 / D, col = i0 % D;
+        for (int base = i0; base < span; base += U * nth) {
+            typename RawOf<FMT>::type v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = base + u * nth;
+                if (i < span) v[u] = load_raw<FMT>(a, lo + i);
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int i = base + u * nth;
+                if (i < span) {
+                    float re, im;
+                    const float2 cst = FMT == RFA_IN_F32_INTERLEAVED ? float2{0.0f, 0.0f} : cs[t];
+                    mix_raw<FMT>(v[u], cst.x, cst.y, re, im);
+                    xs[row * Dp + col] = v2f{re, im};
+                }
+                t += step;
+                if (t >= a.L) t -= a.L;
+                row += srow;
+                col += scol;
+                if (col >= D) col -= D, row++;
+            }
         }
         __syncthreads();
         if (valid) {
-            const v2f *x = xs + (int)(jb + (long long)tid * a.D - lo);
+            // tap k reads staged sample tid*D + rel, rel = k1-1-k
+            int k = k0;
+            while (k < k1) {
+                const int rel = k1 - 1 - k;
+                const int r = rel / D, c = rel - r * D;
+                const int seg = a.pad ? min(c + 1, k1 - k) : k1 - k;   // odd D: rows are contiguous
+                const v2f *x = xs + (tid + r) * Dp + c;
+                const float *w = wl + (k - k0);
 #pragma unroll 8
-            for (int k = k0; k < k1; k++) {
-                const float w = a.taps[k];
-                acc = acc + w * x[-k];
+                for (int u = 0; u < seg; u++) acc = acc + w[u] * x[-u];
+                k += seg;
             }
         }
         __syncthreads();
@@ -160,7 +222,7 @@ hipError_t launch_ddc(const DdcLaunch &a, hipStream_t st) {
         static bool attr_set = false;
         if (!attr_set) {
             hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(ddc_fir_kernel<FMT>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, kDynLds);
             if (e != hipSuccess) return e;
             attr_set = true;
         }
@@ -345,21 +407,30 @@ int rebuild_filter(rfa_ddc *d) {
 // output lanes be resident per CU (LDS and wave limits); P = 1 with the taps
 // split into LDS-sized chunks when even one output's window does not fit.
 void plan_tiles(DdcLaunch &a) {
-    const long long cap = kLdsBytes / (long long)sizeof(float2);
+    a.pad = (a.D & 1) ? 0 : 1;
+    const long long Dp = a.D + a.pad;
+    // dynamic LDS of a workgroup: kc taps (padded to 4) + rows of staged samples
+    auto lds_of = [&](int P, long long kc) {
+        const long long span = (long long)(P - 1) * a.D + kc;
+        return (span + a.D - 1) / a.D * Dp * (long long)sizeof(float2) + (kc + 3) / 4 * 16;
+    };
     int best_p = 1, best_lanes = -1;
     for (int P = 1; P <= kThreads; P++) {
-        const long long span = (long long)(P - 1) * a.D + a.T;
-        if (span > cap) break;
+        const long long lds = lds_of(P, a.T);
+        if (lds > kDynLds) break;
         const int threads = (P + 63) / 64 * 64;
-        const int by_lds = (int)(kLdsBytes / (span * (long long)sizeof(float2)));
+        const int by_lds = (int)(kLdsBytes / (lds + kMaxTable * 8));
         const int blocks = std::min(by_lds, kMaxWavesPerCu / (threads / 64));
         const int lanes = P * blocks;
         if (lanes >= best_lanes) best_lanes = lanes, best_p = P;
     }
     a.P = best_p;
     a.threads = (best_p + 63) / 64 * 64;
-    a.KC = (int)std::min<long long>(a.T, cap - (long long)(a.P - 1) * a.D);
-    a.lds_bytes = (int)(((long long)(a.P - 1) * a.D + a.KC) * (long long)sizeof(float2));
+    long long kc = a.T;                     // all taps in one pass when they fit, else chunks
+    while (kc > 1 && lds_of(a.P, kc) > kDynLds) kc = std::max(1LL, kc - a.D);
+    a.KC = (int)kc;
+    a.kc_pad = (a.KC + 3) / 4 * 4;
+    a.lds_bytes = (int)lds_of(a.P, a.KC);
 }
 
 template <int FMT>
