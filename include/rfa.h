@@ -254,6 +254,17 @@ typedef struct rfa_ddc rfa_ddc;
  * the reference's filter design returns null. */
 RFA_API int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
                            rfa_ddc **out);
+/* The same front end with the resampler the live app uses instead of the
+ * Decimator (analyzer/Resampler.kt:102-110, dsp/RationalResampler.kt): the
+ * ratio out/in reduced by limitDenominator(out, in, 10000), polyphase bank
+ * from designResamplerTaps (Kaiser beta 7, fractionalBw 0.4, 500 taps per phase
+ * at most), outputs in the reference's phase order.  Downsampling only
+ * (RFA_ERR_UNSUPPORTED otherwise, as the reference's TODO states).
+ * rfa_ddc_get_taps returns the prototype padded to a multiple of the
+ * interpolation; rfa_ddc_get_ratio the reduced interpolation/decimation. */
+RFA_API int rfa_ddc_create_resampler(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
+                                     rfa_ddc **out);
+RFA_API int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimation, int32_t *taps_per_output);
 RFA_API int rfa_ddc_destroy(rfa_ddc *d);
 RFA_API const char *rfa_ddc_last_error(const rfa_ddc *d);
 /* Like IQConverter.setSampleRate + the Decimator's rebuild check: the mixer
@@ -282,6 +293,11 @@ RFA_API int rfa_ddc_get_mixer(const rfa_ddc *d, float *cos_t, float *sin_t, size
                               int32_t *mix_frequency, int32_t *cosine_index);
 /* Host-only filter design, FirFilter.createLowPassTaps with a Blackman window
  * (no device work).  *num_taps is always set; taps written when it fits. */
+/* Host-only RationalResampler design: limitDenominator + designResamplerTaps
+ * (RationalResampler.kt:165-235); the prototype taps before the polyphase split. */
+RFA_API int rfa_resampler_design(int32_t output_rate, int32_t input_rate, int32_t max_denominator, float fractional_bw,
+                                 int32_t max_taps, int32_t *interpolation, int32_t *decimation, float *taps,
+                                 size_t capacity, int32_t *num_taps);
 RFA_API int rfa_lowpass_taps(float gain, float sample_rate, float cutoff, float transition, float attenuation,
                              int32_t max_taps, float *taps, size_t capacity, int32_t *num_taps);
 

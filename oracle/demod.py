@@ -286,3 +286,202 @@ class CFrontEnd(FrontEnd):
                                   ptr(self.fir.taps), len(self.fir.taps), self.d, ptr(self._dre), ptr(self._dim),
                                   self._ctr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr(ore), ptr(oim))
         return ore[:k], oim[:k]
+
+
+# ---------------------------------------------------------------- RationalResampler
+# dsp/RationalResampler.kt (the resampler the live app's Demodulator uses through
+# analyzer/Resampler.kt:102-110: limitDenominator(out, in, 10000), maxTaps 500).
+
+def gcd(a: int, b: int) -> int:
+    x, y = abs(a), abs(b)
+    while y != 0:
+        x, y = y, x % y
+    return x
+
+
+def limit_denominator(num: int, den: int, max_den: int = 10000):
+    """RationalResampler.limitDenominator (RationalResampler.kt:165-203)."""
+    target = num / den
+    g0 = gcd(num, den)
+    if den // g0 <= max_den:
+        return num // g0, den // g0
+    ln, ld, un, ud = 0, 1, 1, 0
+    while True:
+        mn, md = ln + un, ld + ud
+        if md > max_den:
+            break
+        if mn / md < target:
+            ln, ld = mn, md
+        else:
+            un, ud = mn, md
+    return (ln, ld) if abs(target - ln / ld) < abs(target - un / ud) else (un, ud)
+
+
+def _izero(x: float) -> float:
+    s, term, half, k = 1.0, 1.0, x / 2.0, 1
+    while True:
+        tmp = half / k
+        term *= tmp * tmp
+        s += term
+        if term < 1e-12:
+            break
+        k += 1
+    return s
+
+
+def kaiser(n: int, N: int, beta: float = 7.0) -> np.float32:
+    """KaiserWindow.value (WindowFunctions.kt:63-80)."""
+    ibeta = 1.0 / _izero(beta)
+    if n == 0 or n == N - 1:
+        return F32(ibeta)
+    inm1 = 1.0 / float(N - 1)
+    temp = 2.0 * n * inm1 - 1.0
+    return F32(_izero(beta * math.sqrt(1.0 - temp * temp)) * ibeta)
+
+
+def low_pass_taps_window(gain, sample_rate, cutoff, transition, attenuation, max_taps, window):
+    """createLowPassTaps with an explicit window function (FirFilter.kt:134-195)."""
+    g, fs, fc, tw, att = (F32(v) for v in (gain, sample_rate, cutoff, transition, attenuation))
+    if fs <= 0.0 or fc <= 0.0 or fc > fs / F32(2) or tw <= 0:
+        return None
+    ntaps = _jtoint(float(att * fs) / (22.0 * float(tw)))
+    if max_taps > 0:
+        ntaps = min(ntaps, max_taps)
+    if ntaps & 1 == 0:
+        ntaps += 1
+    pi = F32(math.pi)
+    taps = np.empty(ntaps, F32)
+    M = (ntaps - 1) // 2
+    fwt0 = F32(F32(F32(2) * pi) * fc) / fs
+    for n in range(-M, M + 1):
+        w = window(n + M, ntaps)
+        if n == 0:
+            taps[n + M] = F32(fwt0 / pi) * w
+        else:
+            taps[n + M] = F32(F32(math.sin(float(F32(n) * fwt0))) / F32(F32(n) * pi)) * w
+    fmax = taps[M]
+    for n in range(1, M + 1):
+        fmax = F32(fmax + F32(2) * taps[n + M])
+    return (taps * F32(g / fmax)).astype(F32)
+
+
+def design_resampler_taps(I: int, D: int, fractional_bw: float = 0.4, max_taps: int = 0):
+    """RationalResampler.designResamplerTaps (RationalResampler.kt:210-235)."""
+    halfband = 0.5
+    fbw = float(F32(fractional_bw))
+    rate = F32(F32(I) / F32(D))
+    if rate >= F32(1.0):
+        tw = F32(halfband - fbw)
+        mid = F32(halfband - float(tw) / 2.0)
+    else:
+        tw = F32(float(rate) * (halfband - fbw))
+        mid = F32(float(rate) * halfband - float(tw) / 2.0)
+    t = low_pass_taps_window(I, I, mid, tw, F32(72.22087), max_taps * I, kaiser)
+    return np.zeros(0, F32) if t is None else t
+
+
+class RationalResampler:
+    """RationalResampler state machine (RationalResampler.kt:27-127).  ``resample``
+    is the closed form used for parity (output n: newest input (n*D)//I, phase
+    (n*D) % I, taps summed in the reference's order); ``resample_literal`` the
+    reference's per-call loop, for small cases."""
+
+    def __init__(self, interpolation: int, decimation: int, max_taps: int = 0, fractional_bw: float = 0.4):
+        if not (0 < fractional_bw < 0.5):
+            fractional_bw = 0.4
+        g = gcd(interpolation, decimation)
+        self.I, self.D = interpolation // g, decimation // g
+        proto = list(design_resampler_taps(self.I, self.D, fractional_bw, max_taps))
+        while len(proto) % self.I:
+            proto.append(F32(0))
+        self.proto = np.array(proto, F32)
+        self.nt = len(proto) // self.I
+        self.bank = np.stack([self.proto[p::self.I] for p in range(self.I)]).astype(F32)   # firTaps[phase][i]
+        self.hist_re = np.zeros(self.nt - 1, F32)
+        self.hist_im = np.zeros(self.nt - 1, F32)
+        self.n_done = self.in_done = 0
+        # literal state
+        self._dre = np.zeros(self.nt, F32)
+        self._dim = np.zeros(self.nt, F32)
+        self._di = 0
+        self._ctr = 0
+
+    def _n_total(self, in_total):
+        lim = in_total * self.I
+        return (lim + self.D - 1) // self.D if lim > 0 else 0
+
+    def resample(self, re, im):
+        re, im = np.asarray(re, F32), np.asarray(im, F32)
+        S, T = len(re), self.nt
+        xre = np.concatenate([self.hist_re, re])
+        xim = np.concatenate([self.hist_im, im])
+        ns = np.arange(self.n_done, self._n_total(self.in_done + S), dtype=np.int64)
+        c = (ns * self.D) // self.I - self.in_done + (T - 1)
+        ph = (ns * self.D) % self.I
+        ore = np.zeros(len(ns), F32)
+        oim = np.zeros(len(ns), F32)
+        for t in range(T):
+            w = self.bank[ph, t]
+            ore = ore + w * xre[c - t]
+            oim = oim + w * xim[c - t]
+        self.hist_re = xre[len(xre) - (T - 1):].copy() if T > 1 else xre[:0]
+        self.hist_im = xim[len(xim) - (T - 1):].copy() if T > 1 else xim[:0]
+        self.n_done += len(ns)
+        self.in_done += S
+        return ore.astype(F32), oim.astype(F32)
+
+    def resample_literal(self, re, im):
+        re, im = np.asarray(re, F32), np.asarray(im, F32)
+        length, nt = len(re), self.nt
+        out_re, out_im = [], []
+        if length == 0:
+            return np.zeros(0, F32), np.zeros(0, F32)
+        consumed, idx = 0, 0
+        self._dre[self._di], self._dim[self._di] = re[0], im[0]
+
+        def advance():
+            nonlocal consumed, idx
+            while self._ctr >= self.I:
+                self._ctr -= self.I
+                idx += 1
+                self._di = self._di + 1 if self._di + 1 < nt else 0
+                consumed += 1
+                if consumed >= length:
+                    break
+                self._dre[self._di], self._dim[self._di] = re[idx], im[idx]
+
+        advance()
+        while consumed < length:
+            a, b = F32(0), F32(0)
+            di = self._di
+            for t in self.bank[self._ctr]:
+                a = F32(a + F32(t * self._dre[di]))
+                b = F32(b + F32(t * self._dim[di]))
+                di = di - 1 if di > 0 else nt - 1
+            out_re.append(a)
+            out_im.append(b)
+            self._ctr += self.D
+            advance()
+        return np.array(out_re, F32), np.array(out_im, F32)
+
+
+class ResamplerFrontEnd(FrontEnd):
+    """Scheduler mix + Resampler (Resampler.kt:102-110) for one channel."""
+
+    def __init__(self, fmt: int, sample_rate: int, output_rate: int):
+        self.fmt, self.sample_rate = fmt, sample_rate
+        i, d = limit_denominator(output_rate, sample_rate, 10000)
+        self.rs = RationalResampler(i, d, max_taps=500)
+        self.cos_freq = None
+        self.cos_t = self.sin_t = None
+        self.cosine_index = 0
+
+    def process(self, raw):
+        if self.fmt == IN_F32_INTERLEAVED:
+            v = np.frombuffer(bytes(raw), F32) if not isinstance(raw, np.ndarray) else raw.view(F32)
+            return self.rs.resample(v[0::2], v[1::2])
+        if len(self.cos_t) == 0:
+            return np.zeros(0, F32), np.zeros(0, F32)
+        re, im = mix(self.fmt, raw, self.cos_t, self.sin_t, self.cosine_index)
+        self.cosine_index = (self.cosine_index + len(re)) % len(self.cos_t)
+        return self.rs.resample(re, im)

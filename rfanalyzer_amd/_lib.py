@@ -115,6 +115,14 @@ def _declare(lib: ctypes.CDLL) -> None:
         # demod front end (rfanalyzer_amd/demod.py)
         "rfa_ddc_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.POINTER(_h)]),
+        "rfa_ddc_create_resampler": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
+                                                    ctypes.POINTER(_h)]),
+        "rfa_ddc_get_ratio": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                             ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_resampler_design": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,
+                                                ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                                                ctypes.POINTER(ctypes.c_int32), _fp, ctypes.c_size_t,
+                                                ctypes.POINTER(ctypes.c_int32)]),
         "rfa_ddc_destroy": (ctypes.c_int, [_h]),
         "rfa_ddc_last_error": (ctypes.c_char_p, [_h]),
         "rfa_ddc_set_sample_rate": (ctypes.c_int, [_h, ctypes.c_int32]),

@@ -48,7 +48,9 @@ struct DdcLaunch {
     const float *cosv, *sinv;
     int L, ci;                     // mixer table length, cosine index of raw[0]
     int D;
-    long long first, n_out;        // first output fires at input `first`
+    long long n0, in0, n_out;      // global index of this call's first output / first input
+    long long off;                 // output n's newest input is (n*Dd + off) / I, phase (n*Dd + off) % I
+    int I, Dd;                     // interpolation, decimation (decimator: 1, D)
     int P, KC;                     // outputs per workgroup, taps per LDS chunk
     int threads, lds_bytes;        // workgroup size (P rounded up to 64), dynamic LDS
     int pad;                       // LDS row pitch D + pad is odd
@@ -132,19 +134,26 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
     const int nth = blockDim.x;
     for (int i = tid; i < a.L; i += nth) cs[i] = float2{a.cosv[i], a.sinv[i]};
     __syncthreads();
-    const int D = a.D, Dp = a.D + a.pad;
+    const int D = a.D, Dp = a.D + a.pad;                   // LDS layout: rows of D samples
     const long long m0 = (long long)blockIdx.x * a.P;
     const int nloc = (int)min((long long)a.P, a.n_out - m0);
-    const long long jb = a.first + m0 * D;                 // input index of output m0
     const bool valid = tid < nloc;
+    // newest input of output n (global indices), RationalResampler / FirFilter counters closed-form
+    const long long nf = a.n0 + m0, nl = nf + (nloc - 1), nt = nf + (valid ? tid : 0);
+    const long long cf = (nf * a.Dd + a.off) / a.I, cl = (nl * a.Dd + a.off) / a.I;
+    const long long pos_t = nt * a.Dd + a.off;
+    const int lane_off = (int)(pos_t / a.I - cf);          // decimator: tid * D
+    const int phase = (int)(pos_t % a.I);
+    const long long jb = cf - a.in0;                        // call-relative input index of output m0
     const int step = a.L > 0 ? nth % a.L : 0;
     const int srow = nth / D, scol = nth % D;
     v2f acc = {0.0f, 0.0f};
     for (int k0 = 0; k0 < a.T; k0 += a.KC) {
         const int k1 = min(a.T, k0 + a.KC);
         const long long lo = jb - (k1 - 1);                 // oldest sample any lane needs
-        const int span = (nloc - 1) * D + (k1 - k0);        // fits the LDS the host sized
-        for (int i = tid; i < k1 - k0; i += nth) wl[i] = a.taps[k0 + i];
+        const int span = (int)(cl - cf) + (k1 - k0);         // fits the LDS the host sized
+        if (a.I == 1)
+            for (int i = tid; i < k1 - k0; i += nth) wl[i] = a.taps[k0 + i];
         // leading samples older than this call come from the history (first workgroups only)
         const int nh = (int)min((long long)span, max(0LL, -lo));
         for (int i = tid; i < nh; i += nth) {
@@ -181,18 +190,29 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
             }
         }
         __syncthreads();
-        if (valid) {
-            // tap k reads staged sample tid*D + rel, rel = k1-1-k
+        if (valid && a.pad) {
+            // decimator, even D: tap k reads staged sample tid*D + rel, rel = k1-1-k, in row segments
             int k = k0;
             while (k < k1) {
                 const int rel = k1 - 1 - k;
                 const int r = rel / D, c = rel - r * D;
-                const int seg = a.pad ? min(c + 1, k1 - k) : k1 - k;   // odd D: rows are contiguous
+                const int seg = min(c + 1, k1 - k);
                 const v2f *x = xs + (tid + r) * Dp + c;
                 const float *w = wl + (k - k0);
 #pragma unroll 8
                 for (int u = 0; u < seg; u++) acc = acc + w[u] * x[-u];
                 k += seg;
+            }
+        } else if (valid) {
+            // linear layout: one contiguous walk; taps shared (I == 1, LDS) or this lane's phase row
+            const v2f *x = xs + lane_off + (k1 - 1 - k0);
+            if (a.I == 1) {
+#pragma unroll 8
+                for (int u = 0; u < k1 - k0; u++) acc = acc + wl[u] * x[-u];
+            } else {
+                const float *w = a.taps + (long long)phase * a.T + k0;
+#pragma unroll 8
+                for (int u = 0; u < k1 - k0; u++) acc = acc + w[u] * x[-u];
             }
         }
         __syncthreads();
@@ -254,8 +274,32 @@ float blackman(int n, int N) {
     return 0.42f - 0.5f * c1 + 0.08f * c2;
 }
 
+// KaiserWindow (WindowFunctions.kt:63-99): izero series as GNU Radio's.
+double kaiser_izero(double x) {
+    double sum = 1.0, term = 1.0;
+    const double half = x / 2.0;
+    for (int k = 1;; k++) {
+        const double tmp = half / k;
+        term *= tmp * tmp;
+        sum += term;
+        if (term < 1e-12) break;
+    }
+    return sum;
+}
+
+float kaiser(int n, int N, double beta) {
+    const double ibeta = 1.0 / kaiser_izero(beta);
+    if (n == 0 || n == N - 1) return (float)ibeta;
+    const double inm1 = 1.0 / (double)(N - 1);
+    const double temp = 2.0 * n * inm1 - 1.0;
+    return (float)(kaiser_izero(beta * std::sqrt(1.0 - temp * temp)) * ibeta);
+}
+
+enum { kWinBlackman = 0, kWinKaiser7 = 1 };
+
 // FirFilter.createLowPassTaps (FirFilter.kt:134-195).  false where it returns null.
-bool design_low_pass(float gain, float fs, float fc, float tw, float att, int max_taps, std::vector<float> &taps) {
+bool design_low_pass(float gain, float fs, float fc, float tw, float att, int max_taps, std::vector<float> &taps,
+                     int window = kWinBlackman) {
     if (fs <= 0.0f || fc <= 0.0f || fc > fs / 2 || tw <= 0.0f) return false;
     int ntaps = jtoint((double)(att * fs) / (22.0 * (double)tw));
     if (max_taps > 0) ntaps = std::min(ntaps, max_taps);
@@ -266,7 +310,7 @@ bool design_low_pass(float gain, float fs, float fc, float tw, float att, int ma
     const int M = (ntaps - 1) / 2;
     const float fwT0 = 2 * pi * fc / fs;
     for (int n = -M; n <= M; n++) {
-        const float w = blackman(n + M, ntaps);
+        const float w = window == kWinKaiser7 ? kaiser(n + M, ntaps, 7.0) : blackman(n + M, ntaps);
         if (n == 0) taps[n + M] = fwT0 / pi * w;
         else taps[n + M] = (float)std::sin((double)((float)n * fwT0)) / ((float)n * pi) * w;
     }
@@ -275,6 +319,53 @@ bool design_low_pass(float gain, float fs, float fc, float tw, float att, int ma
     const float g = gain / fmx;
     for (float &t : taps) t *= g;
     return true;
+}
+
+int gcd_i(int a, int b) {  // RationalResampler.gcd
+    int x = std::abs(a), y = std::abs(b);
+    while (y != 0) {
+        const int t = y;
+        y = x % y;
+        x = t;
+    }
+    return x;
+}
+
+// RationalResampler.limitDenominator (RationalResampler.kt:165-203).
+void limit_denominator(int num, int den, int max_den, int &out_i, int &out_d) {
+    const double target = (double)num / (double)den;
+    const int g0 = gcd_i(num, den);
+    if (den / g0 <= max_den) {
+        out_i = num / g0;
+        out_d = den / g0;
+        return;
+    }
+    int ln = 0, ld = 1, un = 1, ud = 0;
+    while (true) {
+        const int mn = ln + un, md = ld + ud;
+        if (md > max_den) break;
+        if ((double)mn / md < target) ln = mn, ld = md;
+        else un = mn, ud = md;
+    }
+    const double le = std::fabs(target - (double)ln / ld), ue = std::fabs(target - (double)un / ud);
+    if (le < ue) out_i = ln, out_d = ld;
+    else out_i = un, out_d = ud;
+}
+
+// RationalResampler.designResamplerTaps (RationalResampler.kt:210-235): Kaiser(7) low-pass at
+// gain = fs = interpolation; empty where createLowPassTaps returns null.
+void design_resampler_taps(int I, int D, float fbw, int max_taps, std::vector<float> &taps) {
+    const double halfband = 0.5;
+    const float rate = (float)I / (float)D;
+    float tw, mid;
+    if (rate >= 1.0f) {
+        tw = (float)(halfband - fbw);
+        mid = (float)(halfband - tw / 2.0);
+    } else {
+        tw = (float)(rate * (halfband - fbw));
+        mid = (float)(rate * halfband - tw / 2.0);
+    }
+    if (!design_low_pass((float)I, (float)I, mid, tw, 72.22087f, max_taps * I, taps, kWinKaiser7)) taps.clear();
 }
 
 // (int)(frequency - channelFrequency) and the fold of generateMixerLookupTable
@@ -335,12 +426,16 @@ struct rfa_ddc {
     int ci = 0;
     std::vector<float> cos_t, sin_t;
     float *d_cos = nullptr;   // [cos 512 | sin 512]
-    // filter (FirFilter state)
-    int D = 0;
-    std::vector<float> taps;
+    // filter: Decimator/FirFilter (mode 0) or Resampler/RationalResampler (mode 1)
+    int mode = 0;
+    int D = 0;                // decimation (mode 1: of the reduced ratio I/D)
+    int I = 1;                // interpolation
+    std::vector<float> taps;  // mode 0: the taps; mode 1: polyphase bank [I][T], phase-major
+    std::vector<float> proto; // mode 1: prototype taps padded to a multiple of I
+    int T = 0;                // taps per output
     float *d_taps = nullptr;
     size_t taps_cap = 0;
-    long long dc = 1;         // decimationCounter (FirFilter.kt:46)
+    long long n_done = 0, in_done = 0;   // outputs produced / inputs consumed since the filter was built
     float *d_hist[2] = {nullptr, nullptr};
     int cur = 0;
     // staging for the _host entry point
@@ -373,45 +468,80 @@ size_t ddc_sample_bytes(int fmt) {
     }
 }
 
-// (Re)build the filter for the current rates: new taps, zeroed delay line,
-// decimationCounter 1 (Decimator.java:177-181, FirFilter.kt:42-46).
+// (Re)build the filter for the current rates with a zeroed delay line:
+// mode 0 Decimator.java:177-181 (decimationCounter 1: first output at input
+// D-1), mode 1 Resampler.kt:102-110 + RationalResampler.kt:27-60 (ctr 0).
 int rebuild_filter(rfa_ddc *d) {
-    std::vector<float> taps;
-    const int D = d->sample_rate / d->out_rate;
-    if (!design_low_pass(1.0f, (float)d->sample_rate, d->out_rate * 0.75f, d->out_rate * 0.25f, 60.0f, 0, taps))
-        return dfail(d, RFA_ERR_INVALID, "low-pass design rejected the rates (createLowPassTaps returns null)");
-    if (D < 1) return dfail(d, RFA_ERR_INVALID, "output rate above input rate");
-    const size_t T = taps.size();
-    if (T > d->taps_cap) {
-        if (d->d_taps) hipFree(d->d_taps);
+    std::vector<float> taps, proto;
+    int I = 1, D, T;
+    if (d->mode == 0) {
+        D = d->sample_rate / d->out_rate;
+        if (!design_low_pass(1.0f, (float)d->sample_rate, d->out_rate * 0.75f, d->out_rate * 0.25f, 60.0f, 0, taps))
+            return dfail(d, RFA_ERR_INVALID, "low-pass design rejected the rates (createLowPassTaps returns null)");
+        if (D < 1) return dfail(d, RFA_ERR_INVALID, "output rate above input rate");
+        T = (int)taps.size();
+    } else {
+        limit_denominator(d->out_rate, d->sample_rate, 10000, I, D);
+        const int g = gcd_i(I, D);
+        I /= g;
+        D /= g;
+        if (I < 1 || D < 1) return dfail(d, RFA_ERR_INVALID, "rate ratio");
+        if (I > D) return dfail(d, RFA_ERR_UNSUPPORTED, "upsampling (the reference resampler only guarantees downsampling)");
+        design_resampler_taps(I, D, 0.4f, 500, proto);
+        if (proto.empty()) return dfail(d, RFA_ERR_INVALID, "resampler design rejected the rates");
+        while (proto.size() % I) proto.push_back(0.0f);
+        T = (int)(proto.size() / I);
+        taps.resize(proto.size());
+        for (int ph = 0; ph < I; ph++)
+            for (int i = 0; i < T; i++) taps[(size_t)ph * T + i] = proto[(size_t)i * I + ph];
+    }
+    const size_t bank = taps.size(), H = (size_t)T;
+    if (bank > d->taps_cap || 2 * H > d->taps_cap * 2) {
+        if (d->d_taps) (void)hipFree(d->d_taps);
         for (float *&h : d->d_hist)
-            if (h) hipFree(h), h = nullptr;
+            if (h) (void)hipFree(h), h = nullptr;
         d->d_taps = nullptr;
         d->taps_cap = 0;
-        if (hipMalloc(&d->d_taps, T * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc taps");
+        const size_t cap = std::max(bank, H);
+        if (hipMalloc(&d->d_taps, cap * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc taps");
         for (float *&h : d->d_hist)
-            if (hipMalloc(&h, 2 * T * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc history");
-        d->taps_cap = T;
+            if (hipMalloc(&h, 2 * cap * sizeof(float)) != hipSuccess) return dfail(d, RFA_ERR_NOMEM, "hipMalloc history");
+        d->taps_cap = cap;
     }
-    DHIP(d, hipMemcpyAsync(d->d_taps, taps.data(), T * sizeof(float), hipMemcpyHostToDevice, d->stream));
-    DHIP(d, hipMemsetAsync(d->d_hist[0], 0, 2 * T * sizeof(float), d->stream));
+    DHIP(d, hipMemcpyAsync(d->d_taps, taps.data(), bank * sizeof(float), hipMemcpyHostToDevice, d->stream));
+    DHIP(d, hipMemsetAsync(d->d_hist[0], 0, 2 * H * sizeof(float), d->stream));
     DHIP(d, hipStreamSynchronize(d->stream));
     d->taps = std::move(taps);
+    d->proto = std::move(proto);
+    d->I = I;
     d->D = D;
-    d->dc = 1;
+    d->T = T;
+    d->n_done = d->in_done = 0;
     d->cur = 0;
     return RFA_OK;
+}
+
+// Offset of the newest-input formula c_n = (n*Dd + off) / I: the decimator's
+// counter starts at 1, so its outputs fire at inputs D-1, 2D-1, ...
+long long out_offset(const rfa_ddc *d) { return d->mode == 0 ? d->D - 1 : 0; }
+
+// Outputs available once `in_total` inputs have been consumed: every n with
+// c_n < in_total (FirFilter.kt:75-98, RationalResampler.kt:80-123).
+long long outputs_for(const rfa_ddc *d, long long in_total) {
+    const long long lim = in_total * d->I - out_offset(d);
+    return lim > 0 ? (lim + d->D - 1) / d->D : 0;
 }
 
 // Outputs per workgroup: the P whose LDS run (P-1)*D + T samples lets the most
 // output lanes be resident per CU (LDS and wave limits); P = 1 with the taps
 // split into LDS-sized chunks when even one output's window does not fit.
 void plan_tiles(DdcLaunch &a) {
-    a.pad = (a.D & 1) ? 0 : 1;
+    a.D = std::max(1, a.Dd / a.I);              // LDS row length (outputs are Dd/I inputs apart)
+    a.pad = (a.I == 1 && !(a.D & 1)) ? 1 : 0;
     const long long Dp = a.D + a.pad;
     // dynamic LDS of a workgroup: kc taps (padded to 4) + rows of staged samples
     auto lds_of = [&](int P, long long kc) {
-        const long long span = (long long)(P - 1) * a.D + kc;
+        const long long span = ((long long)(P - 1) * a.Dd + a.I - 1) / a.I + 1 + kc;
         return (span + a.D - 1) / a.D * Dp * (long long)sizeof(float2) + (kc + 3) / 4 * 16;
     };
     int best_p = 1, best_lanes = -1;
@@ -456,7 +586,8 @@ int rfa_lowpass_taps(float gain, float sample_rate, float cutoff, float transiti
     return RFA_OK;
 }
 
-int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate, rfa_ddc **out) {
+static int ddc_create(int mode, int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
+                      rfa_ddc **out) {
     if (!out) return RFA_ERR_INVALID;
     *out = nullptr;
     if (ddc_sample_bytes(input_format) == 0 || sample_rate <= 0 || output_sample_rate <= 0) return RFA_ERR_INVALID;
@@ -466,6 +597,7 @@ int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t ou
     rfa_ddc *d = new (std::nothrow) rfa_ddc();
     if (!d) return RFA_ERR_NOMEM;
     d->device = device;
+    d->mode = mode;
     d->fmt = input_format;
     d->sample_rate = sample_rate;
     d->out_rate = output_sample_rate;
@@ -481,6 +613,48 @@ int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t ou
         return rc;
     }
     *out = d;
+    return RFA_OK;
+}
+
+int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate, rfa_ddc **out) {
+    return ddc_create(0, device, input_format, sample_rate, output_sample_rate, out);
+}
+
+int rfa_ddc_create_resampler(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
+                             rfa_ddc **out) {
+    return ddc_create(1, device, input_format, sample_rate, output_sample_rate, out);
+}
+
+int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimation, int32_t *taps_per_output) {
+    if (!d) return RFA_ERR_INVALID;
+    if (interpolation) *interpolation = d->I;
+    if (decimation) *decimation = d->D;
+    if (taps_per_output) *taps_per_output = d->T;
+    return RFA_OK;
+}
+
+int rfa_resampler_design(int32_t output_rate, int32_t input_rate, int32_t max_denominator, float fractional_bw,
+                         int32_t max_taps, int32_t *interpolation, int32_t *decimation, float *taps, size_t capacity,
+                         int32_t *num_taps) {
+    if (output_rate <= 0 || input_rate <= 0 || max_denominator <= 0 || !interpolation || !decimation || !num_taps)
+        return RFA_ERR_INVALID;
+    int I, D;
+    limit_denominator(output_rate, input_rate, max_denominator, I, D);
+    const int g = gcd_i(I, D);
+    if (I <= 0 || D <= 0 || g == 0) return RFA_ERR_INVALID;
+    I /= g;
+    D /= g;
+    if (fractional_bw <= 0 || fractional_bw >= 0.5f) fractional_bw = 0.4f;   // RationalResampler.kt:35-37
+    std::vector<float> t;
+    design_resampler_taps(I, D, fractional_bw, max_taps, t);
+    *interpolation = I;
+    *decimation = D;
+    *num_taps = (int32_t)t.size();
+    if (t.empty()) return RFA_ERR_INVALID;
+    if (taps) {
+        if (capacity < t.size()) return RFA_ERR_SIZE;
+        std::memcpy(taps, t.data(), t.size() * sizeof(float));
+    }
     return RFA_OK;
 }
 
@@ -505,7 +679,9 @@ int rfa_ddc_set_sample_rate(rfa_ddc *d, int32_t sample_rate) {
     const int32_t old = d->sample_rate;
     d->sample_rate = sample_rate;
     d->mixer_valid = false;                      // IQConverter.setSampleRate: cosineFrequency = -1
-    if (sample_rate / d->out_rate != d->D) {
+    // Decimator: rebuilt only when the integer decimation changes (Decimator.java:177-178);
+    // Resampler: whenever the input rate changes (Resampler.kt:102)
+    if (d->mode == 1 || sample_rate / d->out_rate != d->D) {
         const int rc = rebuild_filter(d);
         if (rc != RFA_OK) {
             d->sample_rate = old;
@@ -548,9 +724,8 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     const bool mixed = d->fmt != RFA_IN_F32_INTERLEAVED;
     if (mixed && !d->mixer_valid) return dfail(d, RFA_ERR_STATE, "rfa_ddc_set_frequencies not called");
     if (mixed && d->cos_t.empty()) return RFA_OK;   // empty table: the reference mixes nothing
-    const long long S = (long long)n_samples, D = d->D;
-    const long long first = (D - d->dc % D) % D;
-    const long long n = first < S ? (S - 1 - first) / D + 1 : 0;
+    const long long S = (long long)n_samples;
+    const long long n = outputs_for(d, d->in_done + S) - d->n_done;
     if ((size_t)n > out_capacity) return dfail(d, RFA_ERR_SIZE, "output capacity too small");
     if (n > 0 && (!out_re || !out_im)) return RFA_ERR_INVALID;
     DHIP(d, hipSetDevice(d->device));
@@ -560,13 +735,16 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     a.hist = d->d_hist[d->cur];
     a.new_hist = d->d_hist[d->cur ^ 1];
     a.taps = d->d_taps;
-    a.T = (int)d->taps.size();
+    a.T = d->T;
     a.cosv = d->d_cos;
     a.sinv = d->d_cos + 512;
     a.L = mixed ? (int)d->cos_t.size() : 0;
     a.ci = d->ci;
-    a.D = (int)D;
-    a.first = first;
+    a.n0 = d->n_done;
+    a.in0 = d->in_done;
+    a.off = out_offset(d);
+    a.I = d->I;
+    a.Dd = d->D;
     a.n_out = n;
     plan_tiles(a);
     a.out_re = out_re;
@@ -580,7 +758,8 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     }
     if (e != hipSuccess) return dfail(d, RFA_ERR_HIP, std::string("ddc launch: ") + hipGetErrorString(e));
     if (a.T > 1) d->cur ^= 1;
-    d->dc = (d->dc + S) % D;
+    d->n_done += n;
+    d->in_done += S;
     if (mixed) d->ci = (int)(((long long)d->ci + S) % (long long)d->cos_t.size());
     *n_out = (size_t)n;
     return RFA_OK;
@@ -593,7 +772,7 @@ int rfa_ddc_process_host(rfa_ddc *d, const void *in, size_t n_samples, float *ou
     if (n_samples == 0) return RFA_OK;
     DHIP(d, hipSetDevice(d->device));
     const size_t bytes = n_samples * ddc_sample_bytes(d->fmt);
-    const size_t D = (size_t)d->D, most = n_samples / D + 1;
+    const size_t most = (size_t)(outputs_for(d, d->in_done + (long long)n_samples) - d->n_done) + 1;
     if (bytes > d->d_in_cap) {
         if (d->d_in) hipFree(d->d_in);
         d->d_in = nullptr;
@@ -636,11 +815,12 @@ int rfa_ddc_get_stream(const rfa_ddc *d, void **stream) {
 
 int rfa_ddc_get_taps(const rfa_ddc *d, float *taps, size_t capacity, int32_t *num_taps, int32_t *decimation) {
     if (!d) return RFA_ERR_INVALID;
-    if (num_taps) *num_taps = (int32_t)d->taps.size();
+    const std::vector<float> &t = d->mode == 0 ? d->taps : d->proto;   // prototype filter as designed
+    if (num_taps) *num_taps = (int32_t)t.size();
     if (decimation) *decimation = d->D;
     if (taps) {
-        if (capacity < d->taps.size()) return RFA_ERR_SIZE;
-        std::memcpy(taps, d->taps.data(), d->taps.size() * sizeof(float));
+        if (capacity < t.size()) return RFA_ERR_SIZE;
+        std::memcpy(taps, t.data(), t.size() * sizeof(float));
     }
     return RFA_OK;
 }

@@ -50,18 +50,24 @@ def create_low_pass_taps(gain: float, sample_rate: float, cutoff_frequency: floa
 class FrontEnd:
     """One demodulated channel: mix + decimate raw IQ on ``device``.
 
+    ``resampler=True`` filters with the live app's Resampler (analyzer/Resampler.kt:
+    RationalResampler of limitDenominator(out, in, 10000), Kaiser taps) instead of the
+    Decimator.
     ``input_format`` "s8" (HackRF), "u8" (RTL-SDR), "s16" (Airspy/HydraSDR) or "f32"
     (already-mixed interleaved floats: the Decimator alone, as ResamplerTest drives it).
     """
 
-    def __init__(self, input_format: str, sample_rate: int, output_sample_rate: int, device: int = 0):
+    def __init__(self, input_format: str, sample_rate: int, output_sample_rate: int, device: int = 0,
+                 resampler: bool = False):
         if input_format not in FORMATS:
             raise ValueError(f"input_format must be one of {sorted(FORMATS)}")
         self.fmt = FORMATS[input_format]
         self.output_sample_rate = output_sample_rate
+        self.resampler = resampler
         h = _lib._h()
-        st = _lib.lib().rfa_ddc_create(device, self.fmt, sample_rate, output_sample_rate, ctypes.byref(h))
-        _lib.check(st, "rfa_ddc_create")
+        create = _lib.lib().rfa_ddc_create_resampler if resampler else _lib.lib().rfa_ddc_create
+        _lib.check(create(device, self.fmt, sample_rate, output_sample_rate, ctypes.byref(h)),
+                   "rfa_ddc_create_resampler" if resampler else "rfa_ddc_create")
         self._h = h
 
     # -- lifetime
@@ -122,8 +128,16 @@ class FrontEnd:
                                         ctypes.byref(n), ctypes.byref(mf), ctypes.byref(ci)), "get_mixer")
         return c, s, mf.value, ci.value
 
+    def ratio(self):
+        """(interpolation, decimation, taps per output) of the filter."""
+        i, d, t = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        self._check(_lib.lib().rfa_ddc_get_ratio(self._h, ctypes.byref(i), ctypes.byref(d), ctypes.byref(t)),
+                    "rfa_ddc_get_ratio")
+        return i.value, d.value, t.value
+
     def max_outputs(self, n_samples: int) -> int:
-        return n_samples // max(self.decimation, 1) + 1
+        i, d, _ = self.ratio()
+        return n_samples * i // max(d, 1) + 2
 
     # -- processing
     def process(self, data, frequency: int | None = None, channel_frequency: int | None = None):

@@ -23,11 +23,13 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-CONFIGS = [  # name, format, input rate, output rate
-    ("rtlsdr_u8_2.4M_to_96k", "u8", 2_400_000, 96_000),
-    ("hackrf_s8_20M_to_384k_wfm", "s8", 20_000_000, 384_000),
-    ("hackrf_s8_20M_to_96k", "s8", 20_000_000, 96_000),
-    ("airspy_s16_10M_to_96k", "s16", 10_000_000, 96_000),
+CONFIGS = [  # name, format, input rate, output rate, resampler (Resampler.kt) instead of Decimator
+    ("rtlsdr_u8_2.4M_to_96k", "u8", 2_400_000, 96_000, False),
+    ("hackrf_s8_20M_to_384k_wfm", "s8", 20_000_000, 384_000, False),
+    ("hackrf_s8_20M_to_96k", "s8", 20_000_000, 96_000, False),
+    ("airspy_s16_10M_to_96k", "s16", 10_000_000, 96_000, False),
+    ("resampler_u8_2.4M_to_96k", "u8", 2_400_000, 96_000, True),
+    ("resampler_s8_20M_to_384k_wfm", "s8", 20_000_000, 384_000, True),
 ]
 BPS = {"s8": 2, "u8": 2, "s16": 4}
 
@@ -45,13 +47,13 @@ def main():
     from rfanalyzer_amd import demod
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(1)
-    for name, fmt, sr, out in CONFIGS:
+    for name, fmt, sr, out, rsmp in CONFIGS:
         if args.only and args.only not in name:
             continue
         S = args.samples
         raw = torch.randint(0, 256, (S * BPS[fmt],), dtype=torch.uint8, device=dev, generator=g)
         torch.cuda.synchronize()
-        fe = demod.FrontEnd(fmt, sr, out)
+        fe = demod.FrontEnd(fmt, sr, out, resampler=rsmp)
         fe.set_frequencies(100_000_000, 100_150_000)
         cap = fe.max_outputs(S)
         re = torch.empty(cap, device=dev)
@@ -64,13 +66,17 @@ def main():
             n_out = fe.process_device(raw.data_ptr(), S, re.data_ptr(), im.data_ptr(), cap)
         fe.synchronize()
         dt = (time.perf_counter() - t0) / args.steps
-        T, D = len(fe.taps), fe.decimation
+        I, D, T = fe.ratio()
         alg_bytes = S * BPS[fmt] + n_out * 8
-        res = {"config": name, "format": fmt, "sample_rate": sr, "output_rate": out, "decimation": D, "taps": T,
+        res = {"config": name, "format": fmt, "sample_rate": sr, "output_rate": out, "interpolation": I, "decimation": D, "taps_per_output": T,
                "samples_per_call": S, "ms_per_call": round(dt * 1e3, 4), "Msps": round(S / dt / 1e6, 1),
                "alg_GBps": round(alg_bytes / dt / 1e9, 1), "TFLOPs": round(4 * T * n_out / dt / 1e12, 2)}
         if args.cpu_seconds > 0:
             from oracle import demod as od
+            if rsmp:
+                print(json.dumps(res), flush=True)
+                fe.close()
+                continue
             cfe = od.CFrontEnd({"s8": od.IN_S8, "u8": od.IN_U8, "s16": od.IN_S16LE}[fmt], sr, out)
             cfe.set_frequencies(100_000_000, 100_150_000)
             chunk = np.random.default_rng(2).integers(0, 256, (1 << 20) * BPS[fmt], dtype=np.uint8)

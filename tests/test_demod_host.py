@@ -136,3 +136,47 @@ def test_c_loop_equals_vectorised_restatement(fmt, sr, out):
         np.testing.assert_array_equal(ra[1].view(np.int32), rb[1].view(np.int32))
         pos += n_s
     assert pos == n
+
+
+@pytest.mark.parametrize("out,inp", [(96_000, 2_400_000), (384_000, 20_000_000), (12_000, 48_000),
+                                     (44_100, 1_000_000)])
+def test_resampler_closed_form_equals_literal_loop(out, inp):
+    """RationalResampler.resample per call (RationalResampler.kt:62-127) == the
+    closed form the kernel uses, across ragged calls."""
+    i, d = od.limit_denominator(out, inp, 10000)
+    a, b = od.RationalResampler(i, d, max_taps=40), od.RationalResampler(i, d, max_taps=40)
+    rng = np.random.default_rng(out)
+    x = rng.standard_normal((2, 4000)).astype(F32)
+    pos, ga, gb = 0, [], []
+    for n in [1, 2, 3, 500, 0, 77, 3417]:
+        ga.append(a.resample(x[0, pos:pos + n], x[1, pos:pos + n]))
+        gb.append(b.resample_literal(x[0, pos:pos + n], x[1, pos:pos + n]))
+        pos += n
+    for k in (0, 1):
+        np.testing.assert_array_equal(np.concatenate([g[k] for g in ga]), np.concatenate([g[k] for g in gb]))
+    assert a.n_done == len(np.concatenate([g[0] for g in gb]))
+
+
+def test_limit_denominator_and_resampler_design():
+    assert od.limit_denominator(96_000, 2_400_000) == (1, 25)
+    assert od.limit_denominator(384_000, 20_000_000) == (12, 625)
+    i, d = od.limit_denominator(1, 10_007 * 3, 10000)               # denominator beyond the limit
+    assert d <= 10000 and i >= 0
+    t = od.design_resampler_taps(1, 25, 0.4, 500)
+    assert len(t) == 501 and abs(float(t.astype(np.float64).sum()) - 1.0) < 1e-4   # gain I at DC
+
+
+def test_library_resampler_design_bit_exact(lib):
+    import ctypes
+    L = lib
+    for out, inp in [(96_000, 2_400_000), (384_000, 20_000_000), (12_000, 48_000)]:
+        i, d, n = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        assert L.rfa_resampler_design(out, inp, 10000, ctypes.c_float(0.4), 500, ctypes.byref(i), ctypes.byref(d),
+                                      None, 0, ctypes.byref(n)) == 0
+        got = np.empty(n.value, np.float32)
+        assert L.rfa_resampler_design(out, inp, 10000, ctypes.c_float(0.4), 500, ctypes.byref(i), ctypes.byref(d),
+                                      got.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), got.size,
+                                      ctypes.byref(n)) == 0
+        wi, wd = od.limit_denominator(out, inp, 10000)
+        assert (i.value, d.value) == (wi, wd)
+        np.testing.assert_array_equal(got.view(np.int32), od.design_resampler_taps(wi, wd, 0.4, 500).view(np.int32))

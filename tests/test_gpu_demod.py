@@ -171,3 +171,38 @@ def test_errors(rfa):
         fe.process(b"\x00" * 64)
     assert e.value.status == _lib.RFA_ERR_STATE
     fe.close()
+
+
+def _run_resampler(fmt, sr, out, sizes, seed, freqs=(433_000_000, 433_120_000)):
+    raw = _raw(fmt, sum(sizes), seed)
+    ref = od.ResamplerFrontEnd(FMT[fmt], sr, out)
+    fe = demod.FrontEnd(fmt, sr, out, resampler=True)
+    ref.set_frequencies(*freqs)
+    fe.set_frequencies(*freqs)
+    i, d, t = fe.ratio()
+    assert (i, d, t) == (ref.rs.I, ref.rs.D, ref.rs.nt)
+    _same(fe.taps, ref.rs.proto)
+    pos = 0
+    for n in sizes:
+        chunk = raw[pos * SB[fmt]:(pos + n) * SB[fmt]]
+        r = ref.process(chunk)
+        g = fe.process(chunk)
+        _same(g[0], r[0])
+        _same(g[1], r[1])
+        pos += n
+    return fe
+
+
+@pytest.mark.parametrize("fmt,sr,out", [("u8", 2_400_000, 96_000),      # 1/25: one phase
+                                        ("s8", 20_000_000, 384_000),    # 12/625: polyphase
+                                        ("s16", 10_000_000, 96_000),    # 12/1250 -> 6/625
+                                        ("f32", 48_000, 12_000)])       # ResamplerTest.kt rates
+def test_resampler_bit_exact(rfa, fmt, sr, out):
+    _run_resampler(fmt, sr, out, [16384, 3, 1, 0, 9000, 40_001], seed=len(fmt) + out).close()
+
+
+def test_resampler_rate_change_rebuilds(rfa):
+    fe = _run_resampler("s8", 2_000_000, 96_000, [5000], seed=1)
+    fe.set_sample_rate(2_400_000)                  # Resampler.kt:102 recreates on any input-rate change
+    assert fe.ratio()[:2] == (1, 25)
+    fe.close()
