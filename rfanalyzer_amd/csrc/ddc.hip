@@ -747,6 +747,7 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     a.Dd = d->D;
     a.n_out = n;
     plan_tiles(a);
+    if ((n + a.P - 1) / a.P > (long long)INT32_MAX) return dfail(d, RFA_ERR_INVALID, "call too large for one grid");
     a.out_re = out_re;
     a.out_im = out_im;
     hipError_t e = hipSuccess;
