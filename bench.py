@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--pool-mib", type=int, default=768, help="input pool size (> Infinity Cache)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget (0 = skip)")
     p.add_argument("--f32-steps", type=int, default=20, help="steps of the float32-input companion run (0 = skip)")
+    p.add_argument("--demod-steps", type=int, default=5,
+                   help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return p.parse_args()
 
@@ -173,6 +175,32 @@ def copy_ceiling(torch, device, mib=1024, iters=10):
     return round(gbps, 1)
 
 
+def demod_companion(torch, device, steps, samples=1 << 26):
+    """§8(f) row 4 beside the headline (never `value`): RTL-SDR u8 2.4 Msps mixed and
+    decimated to the 96 kHz quadrature rate (Decimator.java:175-191), raw bytes
+    resident in HBM, wall clock over `steps` calls of rfa_ddc_process."""
+    from rfanalyzer_amd import demod
+    raw = torch.randint(0, 256, (2 * samples,), dtype=torch.uint8, device=device)
+    fe = demod.FrontEnd("u8", 2_400_000, 96_000, device=device.index or 0)
+    fe.set_frequencies(100_000_000, 100_150_000)
+    cap = fe.max_outputs(samples)
+    re = torch.empty(cap, device=device)
+    im = torch.empty(cap, device=device)
+    torch.cuda.synchronize()
+    fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
+    fe.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
+    fe.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    _, d, t = fe.ratio()
+    fe.close()
+    return {"workload": "u8 2.4 Msps -> 96 kHz, mix + 273-tap decimating FIR (D 25)", "value": round(samples / dt / 1e6, 1),
+            "unit": "Msamples/s", "ms_per_call": round(dt * 1e3, 4), "samples_per_call": samples, "decimation": d,
+            "taps": t}
+
+
 def main():
     args = parse()
     import torch
@@ -284,6 +312,8 @@ def main():
                          "roofline_achieved_GBps": round(alg32 / (k32 * 1e-3) / 1e9, 1),
                          "roofline_frac": round(alg32 / (k32 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "alg_bytes_per_launch": alg32}
+    if rank == 0 and world == 1 and args.demod_steps > 0:
+        result["demod"] = demod_companion(torch, device, args.demod_steps)
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds, min(16, os.cpu_count() or 1))
     if rank == 0:

@@ -14,13 +14,13 @@ timeout -k 10 420 python bench.py $EXTRA > gpurun_out/bench_$TAG.json 2> gpurun_
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json; tail -3 gpurun_out/bench_$TAG.err; fatal $rc && exit $rc
 rm -rf gpurun_out/prof_$TAG gpurun_out/pmcf_$TAG gpurun_out/pmcw_$TAG
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
-    python3 bench.py --cpu-seconds 0 --f32-steps 0 $EXTRA > gpurun_out/prof_$TAG.log 2>&1
+    python3 bench.py --cpu-seconds 0 --f32-steps 0 --demod-steps 0 $EXTRA > gpurun_out/prof_$TAG.log 2>&1
 rc=$?; echo "rocprof stats rc=$rc"; fatal $rc && { tail -5 gpurun_out/prof_$TAG.log; exit $rc; }
 find gpurun_out/prof_$TAG -name "*kernel_stats.csv" -exec cat {} \;
 timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmcf_$TAG -o run -- \
-    python3 bench.py --cpu-seconds 0 --f32-steps 0 --steps 5 --warmup 1 $EXTRA > gpurun_out/pmcf_$TAG.log 2>&1
+    python3 bench.py --cpu-seconds 0 --f32-steps 0 --demod-steps 0 --steps 5 --warmup 1 $EXTRA > gpurun_out/pmcf_$TAG.log 2>&1
 rc=$?; echo "pmc fetch rc=$rc"; fatal $rc && { tail -5 gpurun_out/pmcf_$TAG.log; exit $rc; }
 timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmcw_$TAG -o run -- \
-    python3 bench.py --cpu-seconds 0 --f32-steps 0 --steps 5 --warmup 1 $EXTRA > gpurun_out/pmcw_$TAG.log 2>&1
+    python3 bench.py --cpu-seconds 0 --f32-steps 0 --demod-steps 0 --steps 5 --warmup 1 $EXTRA > gpurun_out/pmcw_$TAG.log 2>&1
 rc=$?; echo "pmc write rc=$rc"; fatal $rc && { tail -5 gpurun_out/pmcw_$TAG.log; exit $rc; }
 exit 0
