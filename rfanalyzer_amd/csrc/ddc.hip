@@ -54,12 +54,22 @@ struct DdcLaunch {
     int P, KC;                     // outputs per workgroup, taps per LDS chunk
     int threads, lds_bytes;        // workgroup size (P rounded up to 64), dynamic LDS
     int pad;                       // LDS row pitch D + pad is odd
+    int vec4;                      // raw buffer aligned for 4-sample loads
     int kc_pad;                    // floats reserved for the chunk's taps (multiple of 4)
     float *out_re, *out_im;
 };
 
 template <int FMT> struct RawOf { using type = unsigned; };
 template <> struct RawOf<RFA_IN_F32_INTERLEAVED> { using type = float2; };
+// Four consecutive samples as one load.
+template <int FMT> struct Raw4Of { using type = uint2; };        // 8-bit I,Q x 4
+template <> struct Raw4Of<RFA_IN_S16LE> { using type = uint4; };  // int16 I,Q x 4
+
+template <int FMT>
+__device__ __forceinline__ unsigned raw4_elem(typename Raw4Of<FMT>::type v, int e) {
+    if constexpr (FMT == RFA_IN_S16LE) return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+    else return ((e < 2 ? v.x : v.y) >> (16 * (e & 1))) & 0xffffu;
+}
 
 // One complex input sample as stored (I,Q bytes / int16 pair / float pair).
 template <int FMT>
@@ -163,30 +173,94 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
         }
         // raw part: U loads in flight per lane before any is converted
         constexpr int U = 8;
-        const int i0 = nh + tid;
-        int t = cos_index(a, lo + i0);
-        int row = i0 / D, col = i0 % D;
-        for (int base = i0; base < span; base += U * nth) {
-            typename RawOf<FMT>::type v[U];
+        bool staged = false;
+        if constexpr (FMT != RFA_IN_F32_INTERLEAVED) {
+            if (a.vec4) {
+                // 4 consecutive samples per load (8 B for 8-bit IQ, 16 B for int16): four
+                // times the bytes in flight of the per-sample loop, which left HBM latency
+                // exposed.  Groups are aligned in the raw buffer; samples outside
+                // [lo + nh, lo + span) are skipped.
+                using R4 = typename Raw4Of<FMT>::type;
+                const long long gA = lo + nh, gB = lo + span;     // gA >= 0 whenever gA < gB
+                const long long q0 = gA >> 2;
+                // whole groups inside the buffer only; the last < 4 samples of the call
+                // (a group that would run past raw[S-1]) go through scalar loads below
+                const long long qend = min((gB + 3) >> 2, a.S >> 2);
+                const int nq = gA < gB ? (int)max(0LL, qend - q0) : 0;
+                const int step4 = (4 * nth) % max(a.L, 1);
+                const int srow4 = (4 * nth) / D, scol4 = (4 * nth) % D;
+                const int i0 = (int)((q0 + tid) * 4 - lo);          // may be negative for the first group
+                int tq = cos_index(a, lo + i0);
+                int rq = (i0 >= 0 ? i0 / D : -((-i0 + D - 1) / D)), cq = i0 - rq * D;
+                for (int qb = tid; qb < nq; qb += U * nth) {
+                    R4 v[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int i = base + u * nth;
-                if (i < span) v[u] = load_raw<FMT>(a, lo + i);
-            }
+                    for (int u = 0; u < U; u++) {
+                        const int q = qb + u * nth;
+                        if (q < nq) v[u] = static_cast<const R4 *>(a.raw)[q0 + q];
+                    }
 #pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int i = base + u * nth;
-                if (i < span) {
-                    float re, im;
-                    const float2 cst = FMT == RFA_IN_F32_INTERLEAVED ? float2{0.0f, 0.0f} : cs[t];
-                    mix_raw<FMT>(v[u], cst.x, cst.y, re, im);
-                    xs[row * Dp + col] = v2f{re, im};
+                    for (int u = 0; u < U; u++) {
+                        const int q = qb + u * nth;
+                        if (q < nq) {
+                            const int ib = (int)((q0 + q) * 4 - lo);
+                            int t = tq, r = rq, c = cq;
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const int i = ib + e;
+                                if (i >= nh && i < span) {
+                                    float re, im;
+                                    const float2 cst = cs[t];
+                                    mix_raw<FMT>(raw4_elem<FMT>(v[u], e), cst.x, cst.y, re, im);
+                                    xs[r * Dp + c] = v2f{re, im};
+                                }
+                                if (++t >= a.L) t = 0;
+                                if (++c >= D) c = 0, r++;
+                            }
+                        }
+                        tq += step4;
+                        if (tq >= a.L) tq -= a.L;
+                        rq += srow4;
+                        cq += scol4;
+                        if (cq >= D) cq -= D, rq++;
+                    }
                 }
-                t += step;
-                if (t >= a.L) t -= a.L;
-                row += srow;
-                col += scol;
-                if (col >= D) col -= D, row++;
+                const long long gt = max(gA, (a.S >> 2) << 2);     // scalar tail [gt, gB)
+                for (long long g = gt + tid; g < gB; g += nth) {
+                    const int i = (int)(g - lo);
+                    float re, im;
+                    ddc_sample<FMT>(a, g, cos_index(a, g), re, im);
+                    xs[(i / D) * Dp + i % D] = v2f{re, im};
+                }
+                staged = true;
+            }
+        }
+        if (!staged) {
+            const int i0 = nh + tid;
+            int t = cos_index(a, lo + i0);
+            int row = i0 / D, col = i0 % D;
+            for (int base = i0; base < span; base += U * nth) {
+                typename RawOf<FMT>::type v[U];
+    #pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int i = base + u * nth;
+                    if (i < span) v[u] = load_raw<FMT>(a, lo + i);
+                }
+    #pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int i = base + u * nth;
+                    if (i < span) {
+                        float re, im;
+                        const float2 cst = FMT == RFA_IN_F32_INTERLEAVED ? float2{0.0f, 0.0f} : cs[t];
+                        mix_raw<FMT>(v[u], cst.x, cst.y, re, im);
+                        xs[row * Dp + col] = v2f{re, im};
+                    }
+                    t += step;
+                    if (t >= a.L) t -= a.L;
+                    row += srow;
+                    col += scol;
+                    if (col >= D) col -= D, row++;
+                }
             }
         }
         __syncthreads();
@@ -747,6 +821,7 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     a.Dd = d->D;
     a.n_out = n;
     plan_tiles(a);
+    a.vec4 = mixed && ((uintptr_t)in % (4 * sb) == 0);
     if ((n + a.P - 1) / a.P > (long long)INT32_MAX) return dfail(d, RFA_ERR_INVALID, "call too large for one grid");
     a.out_re = out_re;
     a.out_im = out_im;

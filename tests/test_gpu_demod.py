@@ -206,3 +206,24 @@ def test_resampler_rate_change_rebuilds(rfa):
     fe.set_sample_rate(2_400_000)                  # Resampler.kt:102 recreates on any input-rate change
     assert fe.ratio()[:2] == (1, 25)
     fe.close()
+
+
+def test_misaligned_device_input_takes_the_per_sample_loads(rfa):
+    """A raw pointer not aligned to 4 samples uses the per-sample staging loop; same bits."""
+    raw_h = _raw("s8", 30_001, 6)
+    raw = _Dev(raw_h.nbytes)
+    raw.put(raw_h)
+    fe = demod.FrontEnd("s8", 2_400_000, 48_000)
+    fe.set_frequencies(100_000_000, 100_070_000)
+    cap = fe.max_outputs(30_000)
+    re, im = _Dev(4 * cap), _Dev(4 * cap)
+    n = fe.process_device(raw.ptr.value + 2, 30_000, re.ptr.value, im.ptr.value, cap)   # one sample in
+    fe.synchronize()
+    ref = od.FrontEnd(od.IN_S8, 2_400_000, 48_000)
+    ref.set_frequencies(100_000_000, 100_070_000)
+    r = ref.process(raw_h[2:])
+    _same(re.get(n), r[0])
+    _same(im.get(n), r[1])
+    for b in (raw, re, im):
+        b.free()
+    fe.close()
