@@ -9,6 +9,10 @@ reference's interfaces for this path:
     processor.FftProcessor     analyzer/FftProcessor.kt
     source.FileIQSource        source/FileIQSource.java (+ Scheduler framing)
     engine.SpectrumEngine      one librfa handle
+    SpectrumEngine.draw_preprocess, scanner   AnalyzerSurface.drawPreprocessing, MainViewModel scanner
+    recording                  Scheduler recording branch, file names, replay metadata
+    demod.FrontEnd             IQConverter.mixPacketIntoSamplePacket + Decimator / Resampler
+    scheduler.Scheduler        analyzer/Scheduler.kt packet fan-out
 
 There is no CPU fallback: without librfa.so or a HIP device, calls raise.
 """
