@@ -35,7 +35,7 @@ constexpr int kThreads = 256;           // largest workgroup
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
 constexpr int kMaxWavesPerCu = 32;
 constexpr int kMaxTable = 512;        // mixer table capacity (> MAX_COSINE_LENGTH)
-constexpr int kDynLds = kLdsBytes - kMaxTable * 8;  // staged samples; the table takes the rest
+constexpr int kDynLds = kLdsBytes;      // taps + mixer table + staged samples, all dynamic
 constexpr int kMaxCosineLength = 500;   // IQConverter.java:39
 
 struct DdcLaunch {
@@ -56,6 +56,7 @@ struct DdcLaunch {
     int pad;                       // LDS row pitch D + pad is odd
     int vec4;                      // raw buffer aligned for 4-sample loads
     int kc_pad;                    // floats reserved for the chunk's taps (multiple of 4)
+    int cs_v2;                     // LDS slots (8 B) of the mixer table, L rounded up to even
     float *out_re, *out_im;
 };
 
@@ -137,9 +138,10 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 template <int FMT>
 __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
     extern __shared__ __attribute__((aligned(16))) v2f dyn[];
-    v2f *xs = dyn + a.kc_pad / 2;                           // [taps of the chunk | staged samples]
+    // [taps of the chunk | mixer table (cos, sin), L entries | staged samples]
     float *wl = reinterpret_cast<float *>(dyn);
-    __shared__ float2 cs[kMaxTable];                        // mixer table (cos, sin)
+    float2 *cs = reinterpret_cast<float2 *>(dyn + a.kc_pad / 2);
+    v2f *xs = dyn + a.kc_pad / 2 + a.cs_v2;
     const int tid = threadIdx.x;
     const int nth = blockDim.x;
     for (int i = tid; i < a.L; i += nth) cs[i] = float2{a.cosv[i], a.sinv[i]};
@@ -614,16 +616,18 @@ void plan_tiles(DdcLaunch &a) {
     a.pad = (a.I == 1 && !(a.D & 1)) ? 1 : 0;
     const long long Dp = a.D + a.pad;
     // dynamic LDS of a workgroup: kc taps (padded to 4) + rows of staged samples
+    a.cs_v2 = (a.L + 1) / 2 * 2;
+    const long long cs_b = a.cs_v2 * 8LL;
     auto lds_of = [&](int P, long long kc) {
         const long long span = ((long long)(P - 1) * a.Dd + a.I - 1) / a.I + 1 + kc;
-        return (span + a.D - 1) / a.D * Dp * (long long)sizeof(float2) + (kc + 3) / 4 * 16;
+        return (span + a.D - 1) / a.D * Dp * (long long)sizeof(float2) + (kc + 3) / 4 * 16 + cs_b;
     };
     int best_p = 1, best_lanes = -1;
     for (int P = 1; P <= kThreads; P++) {
         const long long lds = lds_of(P, a.T);
         if (lds > kDynLds) break;
         const int threads = (P + 63) / 64 * 64;
-        const int by_lds = (int)(kLdsBytes / (lds + kMaxTable * 8));
+        const int by_lds = (int)(kLdsBytes / lds);
         const int blocks = std::min(by_lds, kMaxWavesPerCu / (threads / 64));
         const int lanes = P * blocks;
         if (lanes >= best_lanes) best_lanes = lanes, best_p = P;
@@ -772,7 +776,7 @@ int rfa_ddc_set_frequencies(rfa_ddc *d, int64_t frequency, int64_t channel_frequ
     if (d->mixer_valid && mf == d->cos_freq) return RFA_OK;
     std::vector<float> c, s;
     mixer_table(d->fmt, d->sample_rate, mf, c, s);
-    if (c.size() > 512) return dfail(d, RFA_ERR_UNSUPPORTED, "mixer table longer than 512");
+    if (c.size() > (size_t)kMaxTable) return dfail(d, RFA_ERR_UNSUPPORTED, "mixer table longer than 512");
     DHIP(d, hipSetDevice(d->device));
     if (!c.empty()) {
         DHIP(d, hipMemcpyAsync(d->d_cos, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice, d->stream));
