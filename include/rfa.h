@@ -25,6 +25,8 @@
  *     ui/MainViewModel.kt:861-929,1391-1540
  *   IQConverter.mixPacketIntoSamplePacket + Decimator      rfa_ddc_*() (demod front end, below)
  *     source/Signed8BitIQConverter.java:53-131, analyzer/Decimator.java:175-191
+ *   Resampler / RationalResampler (live demod path)        rfa_ddc_create_resampler()
+ *     analyzer/Resampler.kt:102-110, dsp/RationalResampler.kt:27-127
  *   (north-star extension) exponential average             rfa_get_ema()
  *     idiom of database/GlobalPerformanceData.kt:44-50
  *
