@@ -206,17 +206,24 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
                         const int q = qb + u * nth;
                         if (q < nq) {
                             const int ib = (int)((q0 + q) * 4 - lo);
-                            int t = tq, r = rq, c = cq;
+                            // the group's four table entries are read before any is used, so
+                            // one LDS round trip covers the group instead of four
+                            float2 cst[4];
+                            int t = tq;
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                cst[e] = cs[t];
+                                if (++t >= a.L) t = 0;
+                            }
+                            int r = rq, c = cq;
 #pragma unroll
                             for (int e = 0; e < 4; e++) {
                                 const int i = ib + e;
                                 if (i >= nh && i < span) {
                                     float re, im;
-                                    const float2 cst = cs[t];
-                                    mix_raw<FMT>(raw4_elem<FMT>(v[u], e), cst.x, cst.y, re, im);
+                                    mix_raw<FMT>(raw4_elem<FMT>(v[u], e), cst[e].x, cst[e].y, re, im);
                                     xs[r * Dp + c] = v2f{re, im};
                                 }
-                                if (++t >= a.L) t = 0;
                                 if (++c >= D) c = 0, r++;
                             }
                         }
