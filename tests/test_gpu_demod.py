@@ -227,3 +227,20 @@ def test_misaligned_device_input_takes_the_per_sample_loads(rfa):
     for b in (raw, re, im):
         b.free()
     fe.close()
+
+
+def test_resampler_rejects_upsampling_and_keeps_state_on_bad_rate(rfa):
+    with pytest.raises(_lib.RfaError) as e:
+        demod.FrontEnd("s8", 48_000, 96_000, resampler=True)     # the reference only guarantees downsampling
+    assert e.value.status == _lib.RFA_ERR_UNSUPPORTED
+    fe = demod.FrontEnd("u8", 2_400_000, 96_000)
+    with pytest.raises(_lib.RfaError):
+        fe.set_sample_rate(100_000)                                # 0.75*96k > fs/2: design fails
+    assert fe.decimation == 25                                     # the old filter is still in place
+    fe.set_frequencies(100_000_000, 100_100_000)
+    raw = _raw("u8", 10_000, 2)
+    ref = od.FrontEnd(od.IN_U8, 2_400_000, 96_000)
+    ref.set_frequencies(100_000_000, 100_100_000)
+    g, r = fe.process(raw), ref.process(raw)
+    _same(g[0], r[0]), _same(g[1], r[1])
+    fe.close()
