@@ -124,6 +124,19 @@ __device__ __forceinline__ int cos_index(const DdcLaunch &a, long long g) {
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 
+// One staged (re, im) pair as its own ds_read_b64.  A volatile LDS access keeps
+// the compiler from fusing neighbours into ds_read2_b64, which moves half the
+// bytes per LDS cycle on gfx950 (MI355X_MICROARCH.md, LDS table); the loads
+// still issue back to back with counted waits (measured 3-9 % faster,
+// profiles/r01o/ddc_unfused_lds_reads_ab.txt).
+__device__ __forceinline__ v2f lds_ld(const v2f *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *(const volatile __attribute__((address_space(3))) v2f *)(p);
+#else
+    return *p;
+#endif
+}
+
 // One lane per decimated output; blockDim = P rounded up to a wave.  The
 // samples all P outputs need for taps [k0, k1) are one contiguous run of
 // (P-1)*D + (k1-k0) samples, staged (converted + mixed) into LDS as (re, im)
@@ -283,7 +296,7 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
                 const v2f *x = xs + (tid + r) * Dp + c;
                 const float *w = wl + (k - k0);
 #pragma unroll 8
-                for (int u = 0; u < seg; u++) acc = acc + w[u] * x[-u];
+                for (int u = 0; u < seg; u++) acc = acc + w[u] * lds_ld(x - u);
                 k += seg;
             }
         } else if (valid) {
@@ -291,11 +304,11 @@ __global__ __launch_bounds__(kThreads) void ddc_fir_kernel(DdcLaunch a) {
             const v2f *x = xs + lane_off + (k1 - 1 - k0);
             if (a.I == 1) {
 #pragma unroll 8
-                for (int u = 0; u < k1 - k0; u++) acc = acc + wl[u] * x[-u];
+                for (int u = 0; u < k1 - k0; u++) acc = acc + wl[u] * lds_ld(x - u);
             } else {
                 const float *w = a.taps + (long long)phase * a.T + k0;
 #pragma unroll 8
-                for (int u = 0; u < k1 - k0; u++) acc = acc + w[u] * x[-u];
+                for (int u = 0; u < k1 - k0; u++) acc = acc + w[u] * lds_ld(x - u);
             }
         }
         __syncthreads();
