@@ -150,6 +150,20 @@ RFA_API int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out);
 RFA_API int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_index);
 RFA_API int rfa_reset_state(rfa_handle *h); /* ring -> -9999, peaks/EMA -> uninitialised */
 
+/* Waterfall speed change (FftProcessor.kt:185-195, waterfallSpeed -> 500/400/300
+ * rows, :103).  As in the reference the ring is rebuilt when the next frame
+ * arrives (inside rfa_process), keeping the history: new row i = old row
+ * (writeIndex + i) % old_rows for i < old_rows, -9999 rows beyond, then
+ * writeIndex = 0.  Until then the old ring, readIndex and writeIndex stay
+ * valid.  ring_rows >= 1; RFA_ERR_INVALID when a boxcar average_length would
+ * not fit.  A ring_rows == 0 handle gains a cleared ring. */
+RFA_API int rfa_set_ring_rows(rfa_handle *h, int32_t ring_rows);
+/* FFT size change (FftProcessor.kt:178-183 ring re-created at -9999 with
+ * writeIndex = 0, :233-236 peaks re-initialised; the EMA restarts): every
+ * per-N table and state buffer is rebuilt for fft_size; tuning, channel range,
+ * stream and ring_rows carry over.  Synchronises. */
+RFA_API int rfa_set_fft_size(rfa_handle *h, int32_t fft_size);
+
 /* Channel signal strength for the squelch (FftProcessor.kt:143-157): for every
  * frame of each rfa_process batch, the mean dB over bins
  * [((start - f0) * (N / sampleRate.toFloat())).toInt(), same for end), each
@@ -266,6 +280,16 @@ RFA_API int rfa_ddc_create(int device, int input_format, int32_t sample_rate, in
  * interpolation; rfa_ddc_get_ratio the reduced interpolation/decimation. */
 RFA_API int rfa_ddc_create_resampler(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
                                      rfa_ddc **out);
+/* A FirFilter with the caller's taps and decimation (dsp/FirFilter.kt:34-110,
+ * e.g. FirFilter.createLowPass): delay line of num_taps zeros, decimationCounter
+ * 1, outputs sum taps[k] * delay[newest - k] with the JVM's separately rounded
+ * products and sums.  input_format as in rfa_ddc_create (RFA_IN_F32_INTERLEAVED:
+ * samples taken as they are; raw formats are mixed first). */
+RFA_API int rfa_ddc_create_fir(int device, int input_format, int32_t sample_rate, const float *taps, int32_t num_taps,
+                               int32_t decimation, rfa_ddc **out);
+/* Enqueue on exactly `stream` (a hipStream_t; NULL restores the handle's own
+ * stream).  Pending work of the previous stream is drained first. */
+RFA_API int rfa_ddc_set_stream(rfa_ddc *d, void *stream);
 RFA_API int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimation, int32_t *taps_per_output);
 RFA_API int rfa_ddc_destroy(rfa_ddc *d);
 RFA_API const char *rfa_ddc_last_error(const rfa_ddc *d);

@@ -181,7 +181,10 @@ class FirDecimator:
         T, S, D = len(self.taps), len(re), self.d
         xre = np.concatenate([self.hist_re, re])
         xim = np.concatenate([self.hist_im, im])
-        first = (D - self.counter) % D if D > 0 else 0
+        # decimationCounter starts at 1 and wraps to 0 when it reaches D (FirFilter.kt:46,101-103):
+        # outputs at inputs with counter == 0, i.e. (counter + j) % D == 0 -- except D = 1,
+        # where the initial 1 is checked once before it becomes 0 (first output at input 1)
+        first = 1 if (D == 1 and self.counter == 1) else ((D - self.counter) % D if D > 0 else 0)
         js = np.arange(first, S, max(D, 1))
         ore = np.zeros(len(js), F32)
         oim = np.zeros(len(js), F32)
@@ -220,9 +223,12 @@ class FrontEnd:
     filter-decimate it.  ``fmt`` IN_F32_INTERLEAVED feeds already-mixed float samples
     straight to the filter (Decimator on a SamplePacket, ResamplerTest.kt:56-62)."""
 
-    def __init__(self, fmt: int, sample_rate: int, output_rate: int):
+    def __init__(self, fmt: int, sample_rate: int, output_rate: int, taps=None, decimation=None):
         self.fmt, self.sample_rate = fmt, sample_rate
-        self.d, taps = decimator_taps(sample_rate, output_rate)
+        if taps is not None:  # a FirFilter(taps, decimation) of the caller's (FirFilter.kt:34-46)
+            self.d = int(decimation)
+        else:
+            self.d, taps = decimator_taps(sample_rate, output_rate)
         if taps is None:
             raise ValueError("filter design rejected the rates")
         self.fir = FirDecimator(taps, self.d)
@@ -253,8 +259,8 @@ class CFrontEnd(FrontEnd):
     orc_ddc_process): second restatement for the tests, scalar CPU baseline for
     scripts/ddc_bench.py."""
 
-    def __init__(self, fmt: int, sample_rate: int, output_rate: int):
-        super().__init__(fmt, sample_rate, output_rate)
+    def __init__(self, fmt: int, sample_rate: int, output_rate: int, taps=None, decimation=None):
+        super().__init__(fmt, sample_rate, output_rate, taps, decimation)
         T = len(self.fir.taps)
         self._dre = np.zeros(T, F32)
         self._dim = np.zeros(T, F32)

@@ -56,8 +56,24 @@ class FftProcessorRef:
         self.ema = None
         self.freq_or_sr_changed = True
 
+    def set_waterfall_rows(self, rows: int) -> None:
+        """waterfallSpeed change: takes effect in the next push (FftProcessor.kt:185-195)."""
+        self.waterfall_rows = rows
+
     def push(self, row: np.ndarray, frequency: int, sample_rate: int) -> None:
         row = np.asarray(row, np.float32)
+        target = getattr(self, "waterfall_rows", self.ring.shape[0])
+        if row.size != self.ring.shape[1]:  # FftProcessor.kt:178-183: new FFT size -> fresh ring
+            self.n = row.size
+            self.ring = np.full((target, row.size), RING_FILL, np.float32)
+            self.write_index = 0
+        if self.ring.shape[0] != target:  # FftProcessor.kt:185-195: resize, history kept
+            old = self.ring
+            new_ring = np.full((target, self.n), RING_FILL, np.float32)
+            for i in range(min(target, old.shape[0])):
+                new_ring[i] = old[(self.write_index + i) % old.shape[0]]
+            self.ring = new_ring
+            self.write_index = 0
         n = self.n
         freq_changed = frequency != self.last_frequency
         sr_changed = sample_rate != self.last_sample_rate
@@ -88,7 +104,7 @@ class FftProcessorRef:
         else:
             self.peaks = None
         if self.ema_alpha is not None:
-            if self.ema is None or self.freq_or_sr_changed:
+            if self.ema is None or self.ema.size != n or self.freq_or_sr_changed:
                 self.ema = row.copy()
             else:
                 reseed = ~(self.ema > -np.inf)

@@ -98,6 +98,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_get_boxcar": (ctypes.c_int, [_h, ctypes.c_int32, _fp]),
         "rfa_get_ring": (ctypes.c_int, [_h, _fp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
         "rfa_reset_state": (ctypes.c_int, [_h]),
+        "rfa_set_ring_rows": (ctypes.c_int, [_h, ctypes.c_int32]),
+        "rfa_set_fft_size": (ctypes.c_int, [_h, ctypes.c_int32]),
         "rfa_get_device_state": (ctypes.c_int, [_h, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
         "rfa_windowed_fft_mag_planar": (ctypes.c_int, [_h, _fp, _fp, _fp, ctypes.c_size_t]),
         "rfa_fft_logmag_interleaved": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t]),
@@ -117,6 +119,9 @@ def _declare(lib: ctypes.CDLL) -> None:
                                           ctypes.POINTER(_h)]),
         "rfa_ddc_create_resampler": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int32,
                                                     ctypes.POINTER(_h)]),
+        "rfa_ddc_create_fir": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int32, _fp, ctypes.c_int32,
+                                              ctypes.c_int32, ctypes.POINTER(_h)]),
+        "rfa_ddc_set_stream": (ctypes.c_int, [_h, _vp]),
         "rfa_ddc_get_ratio": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
                                              ctypes.POINTER(ctypes.c_int32)]),
         "rfa_resampler_design": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_float,

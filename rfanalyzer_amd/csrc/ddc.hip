@@ -34,7 +34,11 @@ namespace {
 constexpr int kThreads = 256;           // largest workgroup
 constexpr int kLdsBytes = 160 * 1024;    // LDS per CU on gfx950
 constexpr int kMaxWavesPerCu = 32;
-constexpr int kMaxTable = 512;        // mixer table capacity (> MAX_COSINE_LENGTH)
+// Mixer tables are sized by their length.  calcOptimalCosineLength
+// (IQConverter.java:64-76) after the fold of generateMixerLookupTable never
+// exceeds MAX_COSINE_LENGTH (an unfolded cycle is sr/|f| < 501 samples, the
+// search stops below 500), but nothing here relies on it: a table only has to
+// fit the LDS beside one staged output window (plan_tiles checks).
 constexpr int kDynLds = kLdsBytes;      // taps + mixer table + staged samples, all dynamic
 constexpr int kMaxCosineLength = 500;   // IQConverter.java:39
 
@@ -514,14 +518,18 @@ struct rfa_ddc {
     int device = 0;
     int fmt = 0;
     int32_t sample_rate = 0, out_rate = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;       // where work is enqueued (own_stream or the caller's)
+    hipStream_t own_stream = nullptr;   // created by the handle; set once rfa_ddc_set_stream is used
     std::string err;
     // mixer (IQConverter state)
     bool mixer_valid = false;
     int32_t cos_freq = 0;
     int ci = 0;
     std::vector<float> cos_t, sin_t;
-    float *d_cos = nullptr;   // [cos 512 | sin 512]
+    float *d_cos = nullptr;   // [cos L | sin L], capacity d_cos_cap entries each
+    size_t d_cos_cap = 0;
+    std::vector<float> fir_taps;  // mode 2: caller's FirFilter taps
+    int fir_decimation = 1;
     // filter: Decimator/FirFilter (mode 0) or Resampler/RationalResampler (mode 1)
     int mode = 0;
     int D = 0;                // decimation (mode 1: of the reduced ratio I/D)
@@ -570,7 +578,11 @@ size_t ddc_sample_bytes(int fmt) {
 int rebuild_filter(rfa_ddc *d) {
     std::vector<float> taps, proto;
     int I = 1, D, T;
-    if (d->mode == 0) {
+    if (d->mode == 2) {  // FirFilter(taps, decimation) as given (FirFilter.kt:34-46)
+        taps = d->fir_taps;
+        D = d->fir_decimation;
+        T = (int)taps.size();
+    } else if (d->mode == 0) {
         D = d->sample_rate / d->out_rate;
         if (!design_low_pass(1.0f, (float)d->sample_rate, d->out_rate * 0.75f, d->out_rate * 0.25f, 60.0f, 0, taps))
             return dfail(d, RFA_ERR_INVALID, "low-pass design rejected the rates (createLowPassTaps returns null)");
@@ -618,8 +630,11 @@ int rebuild_filter(rfa_ddc *d) {
 }
 
 // Offset of the newest-input formula c_n = (n*Dd + off) / I: the decimator's
-// counter starts at 1, so its outputs fire at inputs D-1, 2D-1, ...
-long long out_offset(const rfa_ddc *d) { return d->mode == 0 ? d->D - 1 : 0; }
+// counter starts at 1, so its outputs fire at inputs D-1, 2D-1, ...; with D = 1
+// the initial 1 is checked once before it wraps to 0, so the first output is at
+// input 1 (FirFilter.kt:46,78,101-103; ApplicationTest.kt testFirFilter2 has 63
+// outputs for 64 inputs).
+long long out_offset(const rfa_ddc *d) { return d->mode == 0 ? (d->D >= 2 ? d->D - 1 : 1) : 0; }
 
 // Outputs available once `in_total` inputs have been consumed: every n with
 // c_n < in_total (FirFilter.kt:75-98, RationalResampler.kt:80-123).
@@ -685,7 +700,7 @@ int rfa_lowpass_taps(float gain, float sample_rate, float cutoff, float transiti
 }
 
 static int ddc_create(int mode, int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
-                      rfa_ddc **out) {
+                      rfa_ddc **out, const float *fir_taps = nullptr, int fir_ntaps = 0, int fir_decimation = 1) {
     if (!out) return RFA_ERR_INVALID;
     *out = nullptr;
     if (ddc_sample_bytes(input_format) == 0 || sample_rate <= 0 || output_sample_rate <= 0) return RFA_ERR_INVALID;
@@ -699,11 +714,13 @@ static int ddc_create(int mode, int device, int input_format, int32_t sample_rat
     d->fmt = input_format;
     d->sample_rate = sample_rate;
     d->out_rate = output_sample_rate;
+    if (mode == 2) {
+        d->fir_taps.assign(fir_taps, fir_taps + fir_ntaps);
+        d->fir_decimation = fir_decimation;
+    }
     int rc = RFA_OK;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess)
         rc = RFA_ERR_HIP;
-    else if (hipMalloc(&d->d_cos, 2 * 512 * sizeof(float)) != hipSuccess)
-        rc = RFA_ERR_NOMEM;
     else
         rc = rebuild_filter(d);
     if (rc != RFA_OK) {
@@ -721,6 +738,25 @@ int rfa_ddc_create(int device, int input_format, int32_t sample_rate, int32_t ou
 int rfa_ddc_create_resampler(int device, int input_format, int32_t sample_rate, int32_t output_sample_rate,
                              rfa_ddc **out) {
     return ddc_create(1, device, input_format, sample_rate, output_sample_rate, out);
+}
+
+int rfa_ddc_create_fir(int device, int input_format, int32_t sample_rate, const float *taps, int32_t num_taps,
+                       int32_t decimation, rfa_ddc **out) {
+    if (!out) return RFA_ERR_INVALID;
+    *out = nullptr;
+    if (!taps || num_taps < 1 || decimation < 1 || sample_rate <= 0) return RFA_ERR_INVALID;
+    return ddc_create(2, device, input_format, sample_rate, std::max(1, sample_rate / decimation), out, taps, num_taps,
+                      decimation);
+}
+
+int rfa_ddc_set_stream(rfa_ddc *d, void *stream) {
+    if (!d) return RFA_ERR_INVALID;
+    // the filter history and mixer uploads are ordered on the handle's stream: drain it first
+    DHIP(d, hipSetDevice(d->device));
+    DHIP(d, hipStreamSynchronize(d->stream));
+    if (d->own_stream == nullptr) d->own_stream = d->stream;
+    d->stream = stream ? (hipStream_t)stream : d->own_stream;
+    return RFA_OK;
 }
 
 int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimation, int32_t *taps_per_output) {
@@ -763,7 +799,8 @@ int rfa_ddc_destroy(rfa_ddc *d) {
     for (void *p : {(void *)d->d_cos, (void *)d->d_taps, (void *)d->d_hist[0], (void *)d->d_hist[1], d->d_in,
                     (void *)d->d_out})
         if (p) hipFree(p);
-    if (d->stream) hipStreamDestroy(d->stream);
+    hipStream_t own = d->own_stream ? d->own_stream : d->stream;
+    if (own) hipStreamDestroy(own);
     delete d;
     return RFA_OK;
 }
@@ -779,7 +816,7 @@ int rfa_ddc_set_sample_rate(rfa_ddc *d, int32_t sample_rate) {
     d->mixer_valid = false;                      // IQConverter.setSampleRate: cosineFrequency = -1
     // Decimator: rebuilt only when the integer decimation changes (Decimator.java:177-178);
     // Resampler: whenever the input rate changes (Resampler.kt:102)
-    if (d->mode == 1 || sample_rate / d->out_rate != d->D) {
+    if (d->mode == 1 || (d->mode == 0 && sample_rate / d->out_rate != d->D)) {
         const int rc = rebuild_filter(d);
         if (rc != RFA_OK) {
             d->sample_rate = old;
@@ -796,11 +833,21 @@ int rfa_ddc_set_frequencies(rfa_ddc *d, int64_t frequency, int64_t channel_frequ
     if (d->mixer_valid && mf == d->cos_freq) return RFA_OK;
     std::vector<float> c, s;
     mixer_table(d->fmt, d->sample_rate, mf, c, s);
-    if (c.size() > (size_t)kMaxTable) return dfail(d, RFA_ERR_UNSUPPORTED, "mixer table longer than 512");
+    if (c.size() * 8 > (size_t)kDynLds / 2) return dfail(d, RFA_ERR_UNSUPPORTED, "mixer table larger than half the LDS");
     DHIP(d, hipSetDevice(d->device));
     if (!c.empty()) {
+        if (c.size() > d->d_cos_cap) {
+            DHIP(d, hipStreamSynchronize(d->stream));
+            if (d->d_cos) (void)hipFree(d->d_cos);
+            d->d_cos = nullptr;
+            d->d_cos_cap = 0;
+            if (hipMalloc(&d->d_cos, 2 * c.size() * sizeof(float)) != hipSuccess)
+                return dfail(d, RFA_ERR_NOMEM, "hipMalloc mixer table");
+            d->d_cos_cap = c.size();
+        }
         DHIP(d, hipMemcpyAsync(d->d_cos, c.data(), c.size() * sizeof(float), hipMemcpyHostToDevice, d->stream));
-        DHIP(d, hipMemcpyAsync(d->d_cos + 512, s.data(), s.size() * sizeof(float), hipMemcpyHostToDevice, d->stream));
+        DHIP(d, hipMemcpyAsync(d->d_cos + d->d_cos_cap, s.data(), s.size() * sizeof(float), hipMemcpyHostToDevice,
+                               d->stream));
         DHIP(d, hipStreamSynchronize(d->stream));
     }
     d->cos_t = std::move(c);
@@ -835,7 +882,7 @@ int rfa_ddc_process(rfa_ddc *d, const void *in, size_t n_samples, float *out_re,
     a.taps = d->d_taps;
     a.T = d->T;
     a.cosv = d->d_cos;
-    a.sinv = d->d_cos + 512;
+    a.sinv = d->d_cos + d->d_cos_cap;
     a.L = mixed ? (int)d->cos_t.size() : 0;
     a.ci = d->ci;
     a.n0 = d->n_done;

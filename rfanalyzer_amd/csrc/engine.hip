@@ -55,6 +55,7 @@ struct rfa_handle {
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
     int ring_rows = 0;
+    int pending_ring_rows = -1;       // rfa_set_ring_rows: applied when the next frame arrives
     int write_index = 0, read_index = 0;
     bool have_rows = false;  // at least one row pushed since the last reset
     float *d_peaks = nullptr;
@@ -576,6 +577,37 @@ int rfa_synchronize(rfa_handle *h) {
     return RFA_OK;
 }
 
+// Waterfall-speed resize (FftProcessor.kt:185-195), done where the reference
+// does it: with the next frame, before the retune shift and the row write.
+static int apply_ring_resize(rfa_handle *h) {
+    const int rn = h->pending_ring_rows;
+    h->pending_ring_rows = -1;
+    if (rn < 0 || rn == h->ring_rows) return RFA_OK;
+    const size_t bytes = (size_t)rn * h->n * sizeof(float);
+    float *nr = nullptr, *nt = nullptr;
+    if (hipMalloc(&nr, bytes) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "ring resize");
+    if (hipMalloc(&nt, bytes) != hipSuccess) {
+        hipFree(nr);
+        return fail(h, RFA_ERR_NOMEM, "ring resize");
+    }
+    hipError_t e = rfa::launch_ring_rotate(h->d_ring, h->ring_rows, nr, rn, h->n, h->write_index, kRingFill, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        hipFree(nr);
+        hipFree(nt);
+        return hip_fail(h, e, "ring resize");
+    }
+    hipFree(h->d_ring);
+    hipFree(h->d_ring_tmp);
+    h->d_ring = nr;
+    h->d_ring_tmp = nt;
+    h->ring_rows = rn;
+    h->cfg.ring_rows = rn;
+    h->write_index = 0;
+    if (h->read_index >= rn) h->read_index = 0;  // rewritten by the frame that triggered the resize
+    return RFA_OK;
+}
+
 static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t stride, float *rows,
                         const float *window, int fmt) {
     const int n = h->n;
@@ -586,6 +618,10 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     if ((uintptr_t)in % al || stride % al) return fail(h, RFA_ERR_INVALID, "input pointer/stride misaligned for format");
     if (n_frames > (size_t)0x7fffffff) return fail(h, RFA_ERR_INVALID, "too many frames");
     if (n_frames == 0) return RFA_OK;
+    if (h->pending_ring_rows >= 0) {
+        int rc = apply_ring_resize(h);
+        if (rc) return rc;
+    }
     const bool need_state = h->d_peaks || h->d_ema;
     // channel mean bins of this tuning (FftProcessor.kt:143-151)
     int chan_first = 0, chan_last = 0;
@@ -922,6 +958,41 @@ int rfa_reset_state(rfa_handle *h) {
     rc = reset_peaks_ema(h);
     if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    return RFA_OK;
+}
+
+int rfa_set_ring_rows(rfa_handle *h, int32_t ring_rows) {
+    if (!h || ring_rows < 1) return RFA_ERR_INVALID;
+    if (h->cfg.avg_mode == RFA_AVG_BOXCAR && h->cfg.avg_length >= ring_rows)
+        return fail(h, RFA_ERR_INVALID, "boxcar average_length does not fit the new ring");
+    h->pending_ring_rows = ring_rows == h->ring_rows ? -1 : ring_rows;
+    return RFA_OK;
+}
+
+int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
+    if (!h) return RFA_ERR_INVALID;
+    if (fft_size == h->n) return RFA_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    rfa_config c = h->cfg;
+    c.fft_size = fft_size;
+    if (h->pending_ring_rows >= 0) c.ring_rows = h->pending_ring_rows;  // the ring is re-created at the new speed
+    rfa_handle *nh = nullptr;
+    rc = rfa_create(&c, &nh);
+    if (rc) return fail(h, rc, "rfa_set_fft_size: rebuilding the handle failed");
+    // carried over: tuning, channel range, caller stream, profiling switch (the
+    // ring, peaks and EMA of the new handle start cleared: FftProcessor.kt:178-183,233-236)
+    nh->have_tuning = h->have_tuning;
+    nh->last_frequency = h->last_frequency;
+    nh->last_sample_rate = h->last_sample_rate;
+    nh->chan_on = h->chan_on;
+    nh->chan_start = h->chan_start;
+    nh->chan_end = h->chan_end;
+    if (h->stream != h->own_stream) nh->stream = h->stream;
+    nh->profile = h->profile;
+    std::swap(*h, *nh);
+    rfa_destroy(nh);  // the old tables and buffers
     return RFA_OK;
 }
 

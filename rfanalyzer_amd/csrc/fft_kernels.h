@@ -139,5 +139,9 @@ hipError_t launch_row_windows(const float *row, const int *lo, const int *hi, in
 hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);
 hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s);
 hipError_t launch_boxcar(const float *ring, int rows, int n, int read_index, int length, float *out, hipStream_t s);
+// Waterfall-speed resize (FftProcessor.kt:185-195): dst[i] = src[(write_index + i) % src_rows]
+// for i < src_rows, fill beyond; dst has dst_rows rows.
+hipError_t launch_ring_rotate(const float *src, int src_rows, float *dst, int dst_rows, int n, int write_index,
+                              float fill, hipStream_t s);
 
 }  // namespace rfa

@@ -595,6 +595,28 @@ hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int 
     return hipGetLastError();
 }
 
+// FftProcessor.kt:185-195: the resized ring keeps the history rotated so the
+// next write (writeIndex = 0) lands on the oldest row.
+__global__ void ring_rotate_kernel(const float *src, int src_rows, float *dst, int n, int write_index, float fill) {
+    const int row = blockIdx.y;
+    const float4 *s4 = row < src_rows
+                           ? reinterpret_cast<const float4 *>(src + (size_t)((write_index + row) % src_rows) * n)
+                           : nullptr;
+    float4 *d4 = reinterpret_cast<float4 *>(dst + (size_t)row * n);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += gridDim.x * blockDim.x)
+        d4[i] = s4 ? s4[i] : make_float4(fill, fill, fill, fill);
+}
+
+hipError_t launch_ring_rotate(const float *src, int src_rows, float *dst, int dst_rows, int n, int write_index,
+                              float fill, hipStream_t s) {
+    if (dst_rows <= 0) return hipSuccess;
+    int bx = (n / 4 + 255) / 256;
+    if (bx > 64) bx = 64;
+    hipLaunchKernelGGL(ring_rotate_kernel, dim3(bx, dst_rows), dim3(256), 0, s, src, src ? src_rows : 0, dst, n,
+                       write_index, fill);
+    return hipGetLastError();
+}
+
 // AnalyzerSurface.kt:710-714 at bin resolution: fp32 sum newest-first, / (L+1).
 __global__ void boxcar_kernel(const float *ring, int rows, int n, int read_index, int length, float *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;

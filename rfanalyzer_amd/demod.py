@@ -58,16 +58,23 @@ class FrontEnd:
     """
 
     def __init__(self, input_format: str, sample_rate: int, output_sample_rate: int, device: int = 0,
-                 resampler: bool = False):
+                 resampler: bool = False, _fir=None):
         if input_format not in FORMATS:
             raise ValueError(f"input_format must be one of {sorted(FORMATS)}")
         self.fmt = FORMATS[input_format]
         self.output_sample_rate = output_sample_rate
         self.resampler = resampler
+        self._stream = None
         h = _lib._h()
-        create = _lib.lib().rfa_ddc_create_resampler if resampler else _lib.lib().rfa_ddc_create
-        _lib.check(create(device, self.fmt, sample_rate, output_sample_rate, ctypes.byref(h)),
-                   "rfa_ddc_create_resampler" if resampler else "rfa_ddc_create")
+        if _fir is not None:  # FirFilter(taps, decimation): see FirFilter below
+            taps, decimation = _fir
+            taps = np.ascontiguousarray(taps, np.float32)
+            _lib.check(_lib.lib().rfa_ddc_create_fir(device, self.fmt, sample_rate, taps.ctypes.data_as(_lib._fp),
+                                                     taps.size, decimation, ctypes.byref(h)), "rfa_ddc_create_fir")
+        else:
+            create = _lib.lib().rfa_ddc_create_resampler if resampler else _lib.lib().rfa_ddc_create
+            _lib.check(create(device, self.fmt, sample_rate, output_sample_rate, ctypes.byref(h)),
+                       "rfa_ddc_create_resampler" if resampler else "rfa_ddc_create")
         self._h = h
 
     # -- lifetime
@@ -162,8 +169,20 @@ class FrontEnd:
                                                ctypes.byref(got)), "rfa_ddc_process")
         return got.value
 
+    def set_stream(self, stream_ptr: int | None) -> None:
+        """Enqueue on exactly this hipStream_t (None: the handle's own stream)."""
+        self._check(_lib.lib().rfa_ddc_set_stream(self._h, stream_ptr or None), "rfa_ddc_set_stream")
+        self._stream = stream_ptr or None
+
     def process_tensor(self, raw, out_re, out_im) -> int:
-        """torch.cuda tensors: raw bytes (uint8/int8/int16/float32, contiguous) -> planar float32 outputs."""
+        """torch.cuda tensors: raw bytes (uint8/int8/int16/float32, contiguous) -> planar float32 outputs.
+        Runs on torch's current stream, so it is ordered after the op that produced ``raw``
+        and before any later torch op that reads the outputs."""
+        import torch
+
+        cur = torch.cuda.current_stream(raw.device).cuda_stream
+        if cur != self._stream:
+            self.set_stream(cur)
         n = raw.numel() * raw.element_size() // BYTES_PER_SAMPLE[self.fmt]
         if out_re.numel() != out_im.numel():
             raise ValueError("out_re and out_im must have the same length")
@@ -177,3 +196,34 @@ class FrontEnd:
         s = _lib._vp()
         self._check(_lib.lib().rfa_ddc_get_stream(self._h, ctypes.byref(s)), "rfa_ddc_get_stream")
         return s.value or 0
+
+
+class FirFilter(FrontEnd):
+    """dsp/FirFilter.kt on the device: ``FirFilter.createLowPass(decimation, gain, sampleRate,
+    cutoff, transition, attenuation)`` (FirFilter.kt:243-263) or explicit taps, then
+    ``filter(re, im)`` with the reference's delay line and decimation counter
+    (FirFilter.kt:63-110) carried across calls.  Already-mixed float samples in."""
+
+    def __init__(self, taps, decimation: int, sample_rate: int = 1, device: int = 0):
+        super().__init__("f32", int(sample_rate), max(1, int(sample_rate) // max(1, int(decimation))), device,
+                         _fir=(taps, int(decimation)))
+
+    @classmethod
+    def createLowPass(cls, decimation: int, gain: float, sample_rate: float, cutoff_frequency: float,  # noqa: N802
+                      transition_width: float, attenuation_db: float, device: int = 0):
+        taps = create_low_pass_taps(gain, sample_rate, cutoff_frequency, transition_width, attenuation_db)
+        if taps is None:
+            return None
+        return cls(taps, decimation, max(1, int(sample_rate)), device)
+
+    @property
+    def numberOfTaps(self) -> int:  # noqa: N802
+        return int(self.taps.size)
+
+    def filter(self, re, im):
+        """Planar float32 in -> (re, im) outputs (FirFilter.filter over a whole packet)."""
+        re = np.asarray(re, np.float32)
+        im = np.asarray(im, np.float32)
+        iq = np.empty(2 * re.size, np.float32)
+        iq[0::2], iq[1::2] = re, im
+        return self.process(iq)

@@ -101,7 +101,14 @@ class SpectrumEngine:
         self._check(_lib.lib().rfa_process(self._h, in_ptr, n_frames, frame_stride, rows_ptr), "rfa_process")
 
     def process_tensor(self, t, n_frames: int | None = None, frame_stride: int = 0, rows=None) -> None:
-        """torch.cuda tensors (uint8/int8/float32 input, float32 rows)."""
+        """torch.cuda tensors (uint8/int8/float32 input, float32 rows).  Enqueued on torch's
+        current stream: ordered after the op that produced ``t`` and before later torch ops
+        that read ``rows``."""
+        import torch
+
+        cur = torch.cuda.current_stream(t.device).cuda_stream
+        if cur != getattr(self, "_torch_stream", None):
+            self.set_stream(cur)
         nbytes = t.numel() * t.element_size()
         if n_frames is None:
             n_frames = self.frames_in(nbytes, frame_stride)
@@ -110,9 +117,11 @@ class SpectrumEngine:
     def set_stream(self, stream_ptr: int | None) -> None:
         """Enqueue on exactly this hipStream_t (0/None = HIP null stream)."""
         self._check(_lib.lib().rfa_set_stream(self._h, stream_ptr or None), "rfa_set_stream")
+        self._torch_stream = stream_ptr or None
 
     def use_own_stream(self) -> None:
         self._check(_lib.lib().rfa_use_own_stream(self._h), "rfa_use_own_stream")
+        self._torch_stream = None
 
     def synchronize(self) -> None:
         self._check(_lib.lib().rfa_synchronize(self._h), "rfa_synchronize")
@@ -138,6 +147,7 @@ class SpectrumEngine:
         return out
 
     def ring(self):
+        self._sync_config()  # a pending ring resize lands with the next batch
         out = np.empty((self.cfg.ring_rows, self.n), np.float32)
         ri, wi = ctypes.c_int32(), ctypes.c_int32()
         self._check(_lib.lib().rfa_get_ring(self._h, _fptr(out), ctypes.byref(ri), ctypes.byref(wi)),
@@ -146,6 +156,19 @@ class SpectrumEngine:
 
     def reset_state(self) -> None:
         self._check(_lib.lib().rfa_reset_state(self._h), "rfa_reset_state")
+
+    def set_ring_rows(self, ring_rows: int) -> None:
+        """Waterfall speed change (FftProcessor.kt:185-195): applied with the next frame, history kept."""
+        self._check(_lib.lib().rfa_set_ring_rows(self._h, int(ring_rows)), "rfa_set_ring_rows")
+
+    def set_fft_size(self, fft_size: int) -> None:
+        """FFT size change (FftProcessor.kt:178-183): ring, peaks and EMA start over at the new N."""
+        self._check(_lib.lib().rfa_set_fft_size(self._h, int(fft_size)), "rfa_set_fft_size")
+        self._sync_config()
+
+    def _sync_config(self) -> None:
+        _lib.lib().rfa_get_config(self._h, ctypes.byref(self.cfg))
+        self.n = self.cfg.fft_size
 
     # -- reference seams (host arrays) ------------------------------------------
     def windowed_fft_mag(self, re: np.ndarray, im: np.ndarray, mag_out: np.ndarray) -> bool:
@@ -199,6 +222,7 @@ class SpectrumEngine:
         Returns (colors [ring_rows][width] uint32 ARGB in ring storage order,
         fft_path_y [width] (NaN where no path point), peaks_y [width] or None,
         (autoscale_min, autoscale_max))."""
+        self._sync_config()
         cmap = np.ascontiguousarray(colormap, dtype=np.uint32)
         p = _lib.RfaDrawParams(int(width), int(fft_height), int(viewport_frequency), int(viewport_sample_rate),
                                float(min_db), float(max_db), int(average_length), int(cmap.size),

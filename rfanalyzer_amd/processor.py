@@ -94,9 +94,26 @@ class FftProcessor:
         if rows.shape[0] and rng:
             for mean in self.engine.channel_means():  # one value per frame, as the reference's per-frame callback
                 self.on_average_signal_strength(float(mean))
-            ns_per_frame = self.n * 1e9 / sample_rate  # FftProcessor.kt:160-161
-            self.perf.updateLoad("FftProcessor", (time.perf_counter_ns() - t0) / (ns_per_frame * rows.shape[0]))
+        # Load metric on every frame, channel range or not (FftProcessor.kt:159-161): the
+        # batch's processing time is shared equally by its frames, and the EMA advances
+        # once per frame as the reference's per-frame call does.
+        if rows.shape[0]:
+            ns_per_frame = self.n * 1e9 / sample_rate
+            sample = (time.perf_counter_ns() - t0) / (ns_per_frame * rows.shape[0])
+            for _ in range(rows.shape[0]):
+                self.perf.updateLoad("FftProcessor", sample)
         return rows
+
+    def setWaterfallSpeed(self, speed: str) -> None:  # noqa: N802
+        """waterfallSpeed (FftProcessor.kt:79,185-195): ring of 500/400/300 rows, history kept,
+        applied with the next frame."""
+        self.engine.set_ring_rows(WATERFALL_SPEED_ROWS[speed])
+
+    def setFftSize(self, fft_size: int) -> None:  # noqa: N802
+        """A source packet of another size (FftProcessor.kt:136-139,178-183): fresh ring, peaks, EMA."""
+        with self.data.lock:
+            self.engine.set_fft_size(fft_size)
+            self.n = fft_size
 
     # -- thread form (FftProcessor.kt:84-96,106-123) --------------------------------
     def start(self) -> None:

@@ -1,10 +1,13 @@
 """CPU: demod front end restatement (oracle/demod.py) and the library's host-side
 filter design (rfa_lowpass_taps).
 
-Parity with the JVM is not pinned by vectors (the reference holds none for this
-branch); it is pinned through the restated per-sample loop of FirFilter.filter
-and the property its own test checks (ResamplerTest.kt:20-116: a 100 Hz tone
-through Decimator 48 kHz -> 12 kHz)."""
+Parity with the JVM is pinned by the reference's own FIR golden vectors
+(ApplicationTest.kt:20-176, testFirFilter / testFirFilter2: JVM outputs of
+createLowPass + FirFilter.filter at a 1e-9 tolerance, tests/golden/
+fir_application_test.json), by the restated per-sample loop of FirFilter.filter,
+and by the property ResamplerTest.kt:20-116 checks (a 100 Hz tone through
+Decimator 48 kHz -> 12 kHz).  The mixer tables and the polyphase resampler have
+no JVM vectors in the reference: parity unpinned beyond the restatement."""
 import numpy as np
 import pytest
 
@@ -180,3 +183,48 @@ def test_library_resampler_design_bit_exact(lib):
         wi, wd = od.limit_denominator(out, inp, 10000)
         assert (i.value, d.value) == (wi, wd)
         np.testing.assert_array_equal(got.view(np.int32), od.design_resampler_taps(wi, wd, 0.4, 500).view(np.int32))
+
+
+# ---------------------------------------------------------------- the reference's FIR golden vectors
+import fir_vectors  # noqa: E402
+
+
+@pytest.mark.parametrize("case", fir_vectors.cases(), ids=lambda c: c["name"])
+def test_restatement_matches_reference_fir_vectors(case):
+    """ApplicationTest.kt testFirFilter / testFirFilter2: createLowPass + FirFilter.filter,
+    JVM outputs at the test's 1e-9 tolerance -- the numpy form, the literal loop and
+    the C loop (orc_ddc_process) of the restatement."""
+    re, im = fir_vectors.inputs(case)
+    taps = od.low_pass_taps(case["gain"], case["sample_rate"], case["cutoff"], case["transition"],
+                            case["attenuation"])
+    d = case["decimation"]
+    fir_vectors.check(case, *od.FirDecimator(taps, d).filter(re, im))
+    fir_vectors.check(case, *od.FirDecimator(taps, d).filter_literal(re, im))
+    # the same samples split into ragged packets: state carries over
+    f = od.FirDecimator(taps, d)
+    parts = [f.filter(re[a:b], im[a:b]) for a, b in ((0, 3), (3, 4), (4, 40), (40, len(re)))]
+    fir_vectors.check(case, np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    iq = np.empty(2 * re.size, F32)
+    iq[0::2], iq[1::2] = re, im
+    fe = od.CFrontEnd(od.IN_F32_INTERLEAVED, int(case["sample_rate"]), int(case["sample_rate"]) // d, taps, d)
+    fir_vectors.check(case, *fe.process(iq.view(np.uint8)))
+
+
+@pytest.mark.parametrize("case", fir_vectors.cases(), ids=lambda c: c["name"])
+def test_library_taps_match_reference_fir_vectors(lib, case):
+    """rfa_lowpass_taps (host C) designs the taps behind those vectors bit for bit."""
+    from rfanalyzer_amd import demod
+    args = (case["gain"], case["sample_rate"], case["cutoff"], case["transition"], case["attenuation"])
+    got, want = demod.create_low_pass_taps(*args), od.low_pass_taps(*args)
+    np.testing.assert_array_equal(got.view(np.int32), want.view(np.int32))
+
+
+@pytest.mark.parametrize("offset,sr", [(25_000, 20_000_000), (4_000, 2_400_000), (1_000, 2_000_000),
+                                       (-1_000, 2_000_000), (39_999, 20_000_000), (0, 2_400_000)])
+def test_mixer_table_length_bound(offset, sr):
+    """calcOptimalCosineLength after generateMixerLookupTable's fold (IQConverter.java:64-76,
+    Signed8BitIQConverter.java:53-57) stays <= MAX_COSINE_LENGTH (500) + 1: an unfolded
+    cycle is < 501 samples and the search stops below 500."""
+    mf = od.mix_frequency(100_000_000 + offset, 100_000_000, sr)
+    n = od.optimal_cosine_length(sr, mf)
+    assert 1 <= n <= 501

@@ -244,3 +244,68 @@ def test_resampler_rejects_upsampling_and_keeps_state_on_bad_rate(rfa):
     g, r = fe.process(raw), ref.process(raw)
     _same(g[0], r[0]), _same(g[1], r[1])
     fe.close()
+
+
+# ---------------------------------------------------------------- the reference's FIR golden vectors on the device
+import fir_vectors  # noqa: E402
+
+
+@pytest.mark.parametrize("case", fir_vectors.cases(), ids=lambda c: c["name"])
+@pytest.mark.parametrize("split", [None, (1, 3, 7, 40)])
+def test_fir_filter_matches_reference_vectors(rfa, case, split):
+    """ApplicationTest.kt:20-176: FirFilter.createLowPass(...).filter(in, out) on the GPU
+    (rfa_ddc_create_fir, pre-mixed f32 input) equals the JVM's outputs within the test's
+    1e-9, whole or in ragged packets (delay line and decimation counter carried over;
+    testFirFilter2 has D = 1: first output at input 1)."""
+    re, im = fir_vectors.inputs(case)
+    f = demod.FirFilter.createLowPass(case["decimation"], case["gain"], case["sample_rate"], case["cutoff"],
+                                      case["transition"], case["attenuation"])
+    assert f is not None and f.numberOfTaps == len(od.low_pass_taps(case["gain"], case["sample_rate"],
+                                                                     case["cutoff"], case["transition"],
+                                                                     case["attenuation"]))
+    if split is None:
+        got = f.filter(re, im)
+    else:
+        bounds = [0, *split, re.size]
+        parts = [f.filter(re[a:b], im[a:b]) for a, b in zip(bounds, bounds[1:])]
+        got = (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
+    fir_vectors.check(case, *got)
+    f.close()
+
+
+@pytest.mark.parametrize("offset,sr", [(25_000, 20_000_000), (4_000, 2_400_000), (1_000, 2_000_000),
+                                       (-1_000, 2_000_000), (39_999, 20_000_000)])
+def test_mixer_tables_near_the_centre_frequency(rfa, offset, sr):
+    """Channels within sr/500 of the centre (the fold case of generateMixerLookupTable)
+    demodulate bit-exact against the restatement (table sizes)."""
+    out = 96_000 if sr < 10_000_000 else 384_000
+    _run_both("s8", sr, out, [50_000, 3, 70_001], seed=offset & 0xffff,
+              freqs=(100_000_000 + offset, 100_000_000))
+
+
+def test_process_tensor_is_ordered_on_torch_stream(rfa):
+    """process_tensor runs on torch's current stream: a torch op producing the input just
+    before, and one reading the outputs just after, see the right data."""
+    import torch
+    raw = _raw("s8", 200_000, 77)
+    want = od.FrontEnd(od.IN_S8, 2_400_000, 96_000)
+    want.set_frequencies(100_000_000, 100_130_000)
+    w_re, w_im = want.process(raw)
+    fe = demod.FrontEnd("s8", 2_400_000, 96_000)
+    fe.set_frequencies(100_000_000, 100_130_000)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        src = torch.from_numpy(raw.copy()).to("cuda", non_blocking=False)
+        big = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+        big.fill_(1)                                    # keeps the stream busy ahead of the copy
+        t = torch.empty_like(src)
+        t.copy_(src)                                    # producer on the current (side) stream
+        cap = fe.max_outputs(200_000)
+        o_re = torch.empty(cap, dtype=torch.float32, device="cuda")
+        o_im = torch.empty(cap, dtype=torch.float32, device="cuda")
+        n = fe.process_tensor(t, o_re, o_im)
+        r_re, r_im = o_re[:n].clone(), o_im[:n].clone()  # consumer on the same stream
+    s.synchronize()
+    _same(r_re.cpu().numpy(), w_re)
+    _same(r_im.cpu().numpy(), w_im)
+    fe.close()

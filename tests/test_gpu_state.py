@@ -151,3 +151,120 @@ def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
         return
     assert got.size == frames
     np.testing.assert_allclose(got, np.array(exp, np.float32), rtol=0, atol=gu.DB_TOL)
+
+
+# ---------------------------------------------------------------- config 3 at its real size
+# BASELINE config 3: N = 65536, EMA + peak-hold, one stream, B frames per launch,
+# ring of 500 rows (waterfall SLOW, FftProcessor.kt:103).  The batch sizes pick
+# every state-kernel form launch_state() has at this N (fft_kernels.hip):
+#   B >= 121 -> state_fused_kernel<16>,  64 <= B < 121 -> <8>,
+#   8 < B < 64 -> partial + combine kernels,  B <= 8 -> the one-thread-per-bin kernel,
+# and whether the rows are read back from the ring (B <= ring rows) or from the
+# staging buffer (B > ring rows).  The prefix makes the ring wrap, so the
+# ring-resident read starts at write_index != 0.  N = 32768 reaches <32>.
+# Model: FftProcessor.kt:222-245 (ring write, reverse order, peak-hold), EMA
+# extension (oracle/processor.py ema_batch).
+
+_CFG3 = {}
+
+
+def _cfg3_rows(n, total, seed):
+    key = (n, total, seed)
+    if key not in _CFG3:
+        data = signals.frames_bytes(n, total, "s8", seed, tones=((0.1, 0.4), (-0.27, 0.02)), noise=0.05,
+                                    drift=0.002)
+        rows = oracle.spectrum_rows(data, oracle.IN_S8, n, total, None, oracle.WIN_BLACKMAN)
+        _CFG3.clear()
+        _CFG3[key] = (data, rows)
+    return _CFG3[key]
+
+
+@pytest.mark.parametrize("n,ring_rows,batches", [
+    (65536, 500, (137, 100, 400)),  # <16> (ring read), <8>, <16> after the wrap
+    (65536, 500, (1, 40, 596)),     # serial, partial+combine, <16> from the staging rows (B > ring)
+    (32768, 300, (300, 45)),        # <32> (ring read), partial+combine
+])
+def test_config3_state_at_size(rfa, n, ring_rows, batches):
+    total = sum(batches)
+    data, rows = _cfg3_rows(n, total, 3)
+    fb = 2 * n
+    alpha = 0.1
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=alpha, peak_hold=True,
+                            ring_rows=ring_rows) as e:
+        e.set_tuning(433_920_000, 20_000_000)
+        f = 0
+        for b in batches:
+            e.process(data[f * fb:(f + b) * fb], b, rows=False)
+            f += b
+            assert gu.db_diff(e.peaks(), rows[:f].max(0)) <= gu.DB_TOL, (b, f)
+            assert gu.db_diff(e.ema(), processor.ema_batch(rows[:f], alpha)) <= gu.DB_TOL, (b, f)
+            ring, ri, wi = e.ring()
+            # frame g (0-based, in arrival order) sits at ring row (-g) mod R (writeIndex-- order)
+            assert ri == (-(f - 1)) % ring_rows and wi == (-f) % ring_rows
+            live = range(max(0, f - ring_rows), f)
+            picks = sorted(set(list(live)[:4] + list(live)[-8:] + list(live)[::97]))
+            assert gu.db_diff(ring[[(-g) % ring_rows for g in picks]], rows[picks]) <= gu.DB_TOL
+            if f < ring_rows:
+                assert np.all(ring[[(-g) % ring_rows for g in range(f, ring_rows)]] == -9999)
+
+
+# ---------------------------------------------------------------- waterfall speed / FFT size change
+@pytest.mark.parametrize("sizes", [(5, 8), (8, 3), (5, 5, 2, 7)])
+def test_ring_resize_keeps_history(rfa, sizes):
+    """FftProcessor.kt:185-195: a speed change rebuilds the ring with the next frame,
+    new row i = old row (writeIndex + i) % old_rows, -9999 beyond, writeIndex = 0."""
+    n = 512
+    total = 6 * len(sizes) + 3
+    data = np.random.default_rng(8).integers(-128, 128, size=2 * n * total, dtype=np.int8).tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, total, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(n, sizes[0], peak_hold=True)
+    with rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=sizes[0]) as e:
+        e.set_tuning(100, 1000)
+        f = 0
+        for k, r in enumerate(sizes):
+            if k:
+                e.set_ring_rows(r)
+                p.set_waterfall_rows(r)
+                ring_before, ri_b, _ = e.ring()  # still the old ring until a frame arrives
+                assert ring_before.shape[0] == sizes[k - 1] and ri_b == p.read_index
+            b = 6 if k < len(sizes) - 1 else 9
+            e.process(data[f * 2 * n:(f + b) * 2 * n], b, rows=False)
+            for g in range(f, f + b):
+                p.push(ref_rows[g], 100, 1000)
+            f += b
+            ring, ri, wi = e.ring()
+            assert ring.shape == p.ring.shape and (ri, wi) == (p.read_index, p.write_index)
+            for row_g, row_p in zip(ring, p.ring):
+                fill = row_p == -9999
+                np.testing.assert_array_equal(row_g[fill], row_p[fill])
+                if (~fill).any():
+                    assert gu.db_diff(row_g[~fill], row_p[~fill]) <= gu.DB_TOL
+        assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL
+
+
+def test_fft_size_change_restarts_ring_and_peaks(rfa):
+    """FftProcessor.kt:178-183 (new size -> fresh -9999 ring, writeIndex 0) and :233-236 (peaks re-initialised)."""
+    data = np.random.default_rng(9).integers(-128, 128, size=2 * 2048 * 8, dtype=np.int8).tobytes()
+    rows_a = oracle.spectrum_rows(data, oracle.IN_S8, 1024, 3, None, oracle.WIN_BLACKMAN)
+    rows_b = oracle.spectrum_rows(data[3 * 2 * 1024:], oracle.IN_S8, 2048, 2, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(1024, 4, peak_hold=True, ema_alpha=0.25)
+    with rfa.SpectrumEngine(1024, "blackman", "s8", avg="ema", ema_alpha=0.25, peak_hold=True, ring_rows=4) as e:
+        e.set_tuning(100_000_000, 2_000_000)
+        e.process(data[: 3 * 2 * 1024], 3, rows=False)
+        for r in rows_a:
+            p.push(r, 100_000_000, 2_000_000)
+        e.set_fft_size(2048)
+        assert e.n == 2048
+        e.process(data[3 * 2 * 1024:3 * 2 * 1024 + 2 * 2 * 2048], 2, rows=False)
+        for r in rows_b:
+            p.push(r, 100_000_000, 2_000_000)
+        ring, ri, wi = e.ring()
+        assert ring.shape == (4, 2048) and (ri, wi) == (p.read_index, p.write_index)
+        for row_g, row_p in zip(ring, p.ring):
+            if np.all(row_p == -9999):
+                assert np.all(row_g == -9999)
+            else:
+                assert gu.db_diff(row_g, row_p) <= gu.DB_TOL
+        assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL
+        assert gu.db_diff(e.ema(), p.ema) <= gu.DB_TOL
+        assert gu.db_diff(e.ema(), processor.ema_batch(rows_b, 0.25)) <= gu.DB_TOL
