@@ -3,23 +3,42 @@
 
 Default workload = BASELINE.json config 3, the one the metric is quoted on
 ("IQ Msamples/s + waterfall lines/s at 64k FFT"): 65536-point FFT, Blackman,
-exponential averaging + peak-hold, synthetic 8-bit signed IQ, one stream per
-GPU, B frames per step written into the device waterfall ring.
+exponential averaging + peak-hold, synthetic 8-bit signed IQ, ring of 500
+rows, one stream per GPU (``--mode streams``).
 
-A step = one rfa_process() call over one batch of B frames already resident in
-HBM (the batch rotates through a pool larger than the 256 MiB Infinity Cache so
-every step streams from HBM).  For N>1 each rank runs its own independent
-stream on its own GPU (weak scaling, no data-path collective); the timed region
-is bracketed by barrier + torch.cuda.synchronize() and the max over ranks is
-reported.  `value` is whole-job throughput in Msamples/s.
+A step = ``--calls-per-step`` consecutive rfa_process() calls, each over one
+batch of B frames already resident in HBM (B = one full ring by default, so a
+step is a run of waterfall-sized batches, each updating ring + peak + EMA as
+FftProcessor does frame by frame).  Batches rotate through a pool larger than
+the 256 MiB Infinity Cache, so every call streams from HBM.  ``value`` is
+whole-job Msamples/s.
+
+Multi-GPU (no data-path collective):
+* ``--mode streams`` (config 5's shape): every rank runs its own independent
+  stream on its own GPU; weak scaling.
+* ``--mode shard`` (config 4): batches of 256 frames x 8192 points; each batch
+  is split into contiguous frame ranges (sharding.frame_range), one per rank;
+  strong scaling (the batch is fixed as N grows).  ``--gather`` also gathers
+  the rows to rank 0 each call (the one real exchange of this mode).
+
+Launch: ``python bench.py --gpus N`` spawns N ranks itself (one process per
+GPU, started before anything touches the GPU, 127.0.0.1 rendezvous); under
+torchrun (WORLD_SIZE set) each process is one rank.  The timed region is
+bracketed by barrier + synchronize on both sides; the max over ranks is
+reported.  ``--dry-run`` replaces the GPU work by a sleep and runs the
+launcher + barrier + max-over-ranks path on gloo (CPU tests).
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -27,31 +46,73 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BPS = {"s8": 2, "u8": 2, "s16": 4, "f32": 8, "f32p": 8}
+METRIC = "IQ Msamples/s + waterfall lines/s at 64k FFT; achieved HBM GB/s vs roofline"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--fft-size", type=int, default=65536)
+    p.add_argument("--mode", default="streams", choices=["streams", "shard"])
+    p.add_argument("--calls-per-step", type=int, default=0,
+                   help="rfa_process calls per step (0 = 250 for streams, 200 for shard: >= 0.5 s timed at 20 steps)")
+    p.add_argument("--fft-size", type=int, default=0, help="0 = 65536 (streams) / 8192 (shard)")
     p.add_argument("--format", default="s8", choices=list(BPS))
     p.add_argument("--window", default="blackman")
-    p.add_argument("--frames", type=int, default=500,
-                   help="frames per step (batch); default one full waterfall ring (500 rows, FftProcessor.kt:103)")
+    p.add_argument("--frames", type=int, default=0,
+                   help="frames per call: 0 = 500 (streams: one full waterfall ring, FftProcessor.kt:103) / 256 (shard)")
     p.add_argument("--avg", default="ema", choices=["none", "ema", "boxcar"])
     p.add_argument("--ema-alpha", type=float, default=0.1)
     p.add_argument("--no-peak", action="store_true")
     p.add_argument("--ring-rows", type=int, default=500)
+    p.add_argument("--gather", action="store_true", help="shard mode: gather every call's rows to rank 0")
     p.add_argument("--pool-mib", type=int, default=768, help="input pool size (> Infinity Cache)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget (0 = skip)")
-    p.add_argument("--f32-steps", type=int, default=20, help="steps of the float32-input companion run (0 = skip)")
+    p.add_argument("--f32-steps", type=int, default=4, help="steps of the float32-input companion run (0 = skip)")
     p.add_argument("--demod-steps", type=int, default=5,
                    help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return p.parse_args()
+    p.add_argument("--dry-run", action="store_true", help="no GPU: launcher / barrier / timing path only (gloo)")
+    a = p.parse_args(argv)
+    if a.fft_size == 0:
+        a.fft_size = 65536 if a.mode == "streams" else 8192
+    if a.frames == 0:
+        a.frames = 500 if a.mode == "streams" else 256
+    if a.calls_per_step == 0:
+        a.calls_per_step = 250 if a.mode == "streams" else 200
+    return a
 
 
+# ----------------------------------------------------------------------------- launcher
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """One child process per GPU (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in its env).  The
+    parent never touches the GPU; it waits for every rank and returns the worst code."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    for i, p in enumerate(procs):
+        code = p.wait()
+        if code != 0 and rc == 0:
+            rc = code
+            for q in procs[i + 1:]:  # a failed rank would leave the others waiting at a barrier
+                if q.poll() is None:
+                    q.terminate()
+    return rc
+
+
+# ----------------------------------------------------------------------------- workload
 def make_pool(torch, n, frames, fmt, pool_mib, seed, device):
     """Synthetic IQ batches on device: slowly drifting tone + complex AWGN."""
     samples = n * frames
@@ -78,35 +139,240 @@ def make_pool(torch, n, frames, fmt, pool_mib, seed, device):
     return pool
 
 
-def max_over_ranks(value: float, world: int, device) -> float:
-    """Slowest rank's time: the timed region ends when the last GPU finishes."""
-    if world <= 1:
-        return value
-    import torch
-    import torch.distributed as dist
+class Ranks:
+    """The process group (or a single process): barrier, max-over-ranks, gather."""
 
-    t = torch.tensor([value], device=device, dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    def __init__(self, dry):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist = torch, dist
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = dry
+        self.device = torch.device("cpu") if dry else torch.device("cuda", self.local)
+        if self.world > 1:
+            dist.init_process_group(backend="gloo" if dry else "nccl")
+
+    def sync(self):
+        if not self.dry:
+            self.torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
+
+    def all_values(self, x: float):
+        """Every rank's value of x (rank order)."""
+        if self.world <= 1:
+            return [x]
+        t = self.torch.tensor([x], device=self.device, dtype=self.torch.float64)
+        parts = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return [float(p.item()) for p in parts]
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
 
 
-def cpu_baseline(args, n, seconds, threads=1):
-    """Reference loop (pffft + restated JVM loops, oracle/_ref) on 1 host core, bounded time."""
+def timed(ranks, step, steps, warmup):
+    """W untimed steps, then EXACTLY `steps` steps between barrier + synchronize on
+    both sides.  Returns (slowest rank's seconds, every rank's seconds)."""
+    for k in range(warmup):
+        step(k)
+    ranks.sync()
+    ranks.barrier()
+    ranks.sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k)
+    ranks.sync()
+    ranks.barrier()
+    ranks.sync()
+    el = time.perf_counter() - t0
+    per = ranks.all_values(el)
+    return max(per), per
+
+
+def run_streams(args, ranks, fmt, steps, warmup, seed):
+    """Config 3 per rank: one stream, B frames per call into ring + peak + EMA.
+    Returns (slowest seconds, per-rank seconds, main-kernel ms per launch, kernel name)."""
+    import rfanalyzer_amd
+
+    torch = ranks.torch
+    n, frames, calls = args.fft_size, args.frames, args.calls_per_step
+    stream = torch.cuda.current_stream(ranks.device)
+    eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
+                                        ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
+                                        ring_rows=args.ring_rows, device=ranks.local)
+    eng.set_stream(stream.cuda_stream)
+    pool = make_pool(torch, n, frames, fmt, args.pool_mib, seed, ranks.device)
+    eng.set_tuning(100_000_000, 20_000_000)
+    ctr = [0]
+
+    ptrs = [b.data_ptr() for b in pool]
+
+    def step(_k):
+        for _ in range(calls):  # rfa_process on the torch stream set above (no per-call Python stream lookup)
+            eng.process_device(ptrs[ctr[0] % len(ptrs)], frames, 0, None)
+            ctr[0] += 1
+
+    for _ in range(warmup):  # untimed, before the kernel clock starts
+        step(0)
+    eng.set_profiling(True)
+    ms0, l0 = eng.kernel_time()
+    slow, per = timed(ranks, step, steps, 0)
+    ms1, l1 = eng.kernel_time()
+    eng.set_profiling(False)
+    name = eng.main_kernel_name()
+    eng.close()
+    del pool
+    return slow, per, (ms1 - ms0) / max(1, l1 - l0), name
+
+
+def run_shard(args, ranks, steps, warmup):
+    """Config 4: every call is one batch of `frames` independent frames split over the
+    ranks (sharding.frame_range); rows stay on each rank's device unless --gather."""
+    import rfanalyzer_amd
+    from rfanalyzer_amd import sharding
+
+    torch = ranks.torch
+    n, frames, fmt, calls = args.fft_size, args.frames, args.format, args.calls_per_step
+    s, e = sharding.frame_range(frames, ranks.rank, ranks.world)
+    mine = e - s
+    stream = torch.cuda.current_stream(ranks.device)
+    eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, ring_rows=0, device=ranks.local)
+    eng.set_stream(stream.cuda_stream)
+    # each rank holds its frame range of every pool batch (host-pinned slices in a
+    # deployment; device-resident here so the timed region measures the GPU path)
+    pool = [b.view(torch.uint8)[s * n * BPS[fmt]:e * n * BPS[fmt]].clone()
+            for b in make_pool(torch, n, frames, fmt, args.pool_mib, 4, ranks.device)]
+    rows = torch.empty(max(1, mine) * n, dtype=torch.float32, device=ranks.device)
+    gathered = None
+    if args.gather and ranks.world > 1:
+        gathered = [torch.empty(((frames + ranks.world - 1) // ranks.world) * n, dtype=torch.float32,
+                                device=ranks.device) for _ in range(ranks.world)]
+        padded = torch.zeros_like(gathered[0])
+    ctr = [0]
+
+    ptrs, rows_ptr = [b.data_ptr() for b in pool], rows.data_ptr()
+
+    def step(_k):
+        for _ in range(calls):
+            if mine:
+                eng.process_device(ptrs[ctr[0] % len(ptrs)], mine, 0, rows_ptr)
+            if gathered is not None:
+                padded[:mine * n].copy_(rows[:mine * n])
+                ranks.dist.all_gather(gathered, padded)
+            ctr[0] += 1
+
+    for _ in range(warmup):
+        step(0)
+    eng.set_profiling(True)
+    ms0, l0 = eng.kernel_time()
+    slow, per = timed(ranks, step, steps, 0)
+    ms1, l1 = eng.kernel_time()
+    eng.set_profiling(False)
+    name = eng.main_kernel_name()
+    eng.close()
+    return slow, per, (ms1 - ms0) / max(1, l1 - l0), name, (s, e)
+
+
+# ----------------------------------------------------------------------------- companions
+def copy_ceiling(torch, device, mib=1024, iters=20):
+    """Device stream-copy ceiling in the same run (SURVEY.md §8(d) primary denominator):
+    librfa's float4 copy kernel (rfa_stream_copy) over two 1 GiB buffers, 2 x bytes / time."""
+    from rfanalyzer_amd import _lib
+
+    L = _lib.lib()
+    src = torch.empty(mib * 2 ** 20 // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    st = torch.cuda.current_stream(device)
+    nb = src.numel() * 4
+    _lib.check(L.rfa_stream_copy(dst.data_ptr(), src.data_ptr(), nb, st.cuda_stream), "rfa_stream_copy")
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(iters):
+        L.rfa_stream_copy(dst.data_ptr(), src.data_ptr(), nb, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(dst[:1024], src[:1024]))
+    gbps = 2 * nb * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    return round(gbps, 1), ok
+
+
+def demod_companion(torch, device, steps, samples=1 << 26):
+    """§8(f) row 4 beside the headline (never `value`): RTL-SDR u8 2.4 Msps mixed and
+    decimated to the 96 kHz quadrature rate (Decimator.java:175-191), raw bytes
+    resident in HBM, wall clock over `steps` calls of rfa_ddc_process."""
+    from rfanalyzer_amd import demod
+    raw = torch.randint(0, 256, (2 * samples,), dtype=torch.uint8, device=device)
+    fe = demod.FrontEnd("u8", 2_400_000, 96_000, device=device.index or 0)
+    fe.set_frequencies(100_000_000, 100_150_000)
+    cap = fe.max_outputs(samples)
+    re = torch.empty(cap, device=device)
+    im = torch.empty(cap, device=device)
+    torch.cuda.synchronize()
+    fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
+    fe.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
+    fe.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    _, d, t = fe.ratio()
+    fe.close()
+    return {"workload": "u8 2.4 Msps -> 96 kHz, mix + 273-tap decimating FIR (D 25)", "value": round(samples / dt / 1e6, 1),
+            "unit": "Msamples/s", "ms_per_call": round(dt * 1e3, 4), "samples_per_call": samples, "decimation": d,
+            "taps": t}
+
+
+def pmc_traffic(args, fmt, n, frames):
+    """roofline.traffic: HBM bytes per launch from the rocprofv3 PMC passes of the
+    committed profile, used only when they were measured on this exact librfa.so."""
+    from rfanalyzer_amd import _lib
+
+    try:
+        with open(args.traffic_file) as fh:
+            tr = json.load(fh)
+    except (OSError, ValueError):
+        return None, "no PMC record"
+    rec = tr.get(f"{fmt}_{n}_{frames}")
+    if not rec:
+        return None, "no PMC record for this workload"
+    with open(_lib.LIB_PATH, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    if rec.get("librfa_sha16") != sha:
+        return None, f"PMC record is for another build ({rec.get('librfa_sha16')}, this {sha})"
+    return rec["hbm_bytes_per_launch"], f"{rec.get('source', args.traffic_file)} (librfa {sha})"
+
+
+# ----------------------------------------------------------------------------- cpu baseline
+def _synthetic_frames(n, frames, fmt, seed=3):
     import numpy as np
-
-    import oracle
-
-    fmt = {"s8": 0, "f32": 3}.get(args.format)
-    frames = max(1, (8 * 2 ** 20) // (n * 8))  # ~8 MB sample, processed repeatedly
-    rng = np.random.Generator(np.random.PCG64(3))
+    rng = np.random.Generator(np.random.PCG64(seed))
     t = np.arange(n * frames)
     x = 0.5 * np.exp(2j * np.pi * 0.07 * t) + 0.05 * (rng.standard_normal(t.size) + 1j * rng.standard_normal(t.size))
     iq = np.empty(2 * t.size)
     iq[0::2], iq[1::2] = x.real, x.imag
-    if fmt == 0 or fmt is None:
-        data, fmt = np.clip(np.rint(iq * 128), -128, 127).astype(np.int8), 0
-    else:
-        data = iq.astype(np.float32)
+    if fmt == 0:
+        return np.clip(np.rint(iq * 128), -128, 127).astype(np.int8)
+    return iq.astype(np.float32)
+
+
+def cpu_baseline(args, n, seconds, threads=1):
+    """Reference loop (pffft + restated JVM loops, oracle/_ref) on host cores, bounded time."""
+    import numpy as np
+
+    import oracle
+
+    fmt = {"s8": 0, "f32": 3}.get(args.format, 0)
+    frames = max(1, (8 * 2 ** 20) // (n * 8))  # ~8 MB sample, processed repeatedly
+    data = _synthetic_frames(n, frames, fmt)
     w = oracle.window(n, oracle.WIN_BLACKMAN)
     ring_rows = 500
     fp = ctypes.POINTER(ctypes.c_float)
@@ -157,169 +423,173 @@ def cpu_baseline(args, n, seconds, threads=1):
     return out
 
 
-def copy_ceiling(torch, device, mib=1024, iters=10):
-    """Device stream-copy ceiling in the same run (SURVEY.md §8(d) primary denominator):
-    torch's copy kernel over two 1 GiB buffers, GB/s = 2 x bytes / time."""
-    src = torch.empty(mib * 2 ** 20 // 4, dtype=torch.float32, device=device).fill_(1.0)
-    dst = torch.empty_like(src)
-    dst.copy_(src)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        dst.copy_(src)
-    e1.record()
-    torch.cuda.synchronize()
-    gbps = 2 * src.numel() * 4 * iters / (e0.elapsed_time(e1) * 1e-3) / 1e9
-    del src, dst
-    return round(gbps, 1)
+def config1_replay(device_ok: bool):
+    """BASELINE config 1: FileIQSource replay of a 1 s 8-bit
+    capture (HackRF s8, 2 Msps, 4 000 000 B, seed 1: tone at +250 kHz, 0.5 FS, AWGN
+    sigma 0.05), N = 1024, no averaging -- host plumbing.  The reference path (packet
+    read FileIQSource.java:318-369, framing Scheduler.kt:252-279, LUT + Blackman +
+    pffft + log-mag + ring, oracle/_ref) and the same replay through librfa
+    (rfa_process_host per packet: PCIe + launch latency) both per frame."""
+    import numpy as np
+
+    import oracle
+    from rfanalyzer_amd import source
+
+    n, sr, nbytes = 1024, 2_000_000, 4_000_000
+    rng = np.random.Generator(np.random.PCG64(1))
+    t = np.arange(nbytes // 2)
+    x = 0.5 * np.exp(2j * np.pi * 250_000 / sr * t) + 0.05 * (rng.standard_normal(t.size) +
+                                                             1j * rng.standard_normal(t.size))
+    iq = np.empty(2 * t.size)
+    iq[0::2], iq[1::2] = x.real, x.imag
+    raw = np.clip(np.rint(iq * 128), -128, 127).astype(np.int8)
+    out = {"workload": "config1: FileIQSource replay, 1 s s8 2 Msps capture, 1024-pt FFT, no averaging"}
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "capture_s8_2msps.iq")
+        raw.tofile(path)
+
+        def replay(per_frame):
+            src = source.FileIQSource()
+            src.init(path, sr, 100_000_000, repeat=False)
+            assert src.open()
+            frames, t0 = 0, time.perf_counter()
+            while True:
+                try:
+                    pkt = src.getPacket()
+                except (EOFError, IOError, OSError):
+                    break
+                if pkt is None:
+                    break
+                per_frame(np.frombuffer(bytes(pkt), np.int8)[:2 * n])
+                frames += 1
+            el = time.perf_counter() - t0
+            src.close()
+            return frames, el
+
+        if oracle.ref_available():
+            lib = oracle.ref()
+            w = oracle.window(n, oracle.WIN_BLACKMAN)
+            ring = np.full((400, n), -9999, np.float32)
+            peaks = np.full(n, -999999, np.float32)
+            fp = ctypes.POINTER(ctypes.c_float)
+
+            def ref_frame(fr):
+                fr = np.ascontiguousarray(fr)
+                assert lib.ref_loop(fr.ctypes.data, 0, n, 1, 2 * n, w.ctypes.data_as(fp), ring.ctypes.data_as(fp),
+                                    400, peaks.ctypes.data_as(fp)) == 0
+
+            frames, el = replay(ref_frame)
+            out["reference"] = {"frames": frames, "us_per_frame": round(el / max(frames, 1) * 1e6, 2), "cores": 1,
+                                "kind": "reference"}
+        if device_ok:
+            import rfanalyzer_amd
+            eng = rfanalyzer_amd.SpectrumEngine(n, "blackman", "s8", ring_rows=400)
+            eng.set_tuning(100_000_000, sr)
+            frames, el = replay(lambda fr: eng.process(fr.tobytes(), 1, rows=True))
+            eng.close()
+            out["librfa_host_buffers"] = {"frames": frames, "us_per_frame": round(el / max(frames, 1) * 1e6, 2),
+                                          "note": "rfa_process_host per packet: launch + PCIe latency bound"}
+    return out
 
 
-def demod_companion(torch, device, steps, samples=1 << 26):
-    """§8(f) row 4 beside the headline (never `value`): RTL-SDR u8 2.4 Msps mixed and
-    decimated to the 96 kHz quadrature rate (Decimator.java:175-191), raw bytes
-    resident in HBM, wall clock over `steps` calls of rfa_ddc_process."""
-    from rfanalyzer_amd import demod
-    raw = torch.randint(0, 256, (2 * samples,), dtype=torch.uint8, device=device)
-    fe = demod.FrontEnd("u8", 2_400_000, 96_000, device=device.index or 0)
-    fe.set_frequencies(100_000_000, 100_150_000)
-    cap = fe.max_outputs(samples)
-    re = torch.empty(cap, device=device)
-    im = torch.empty(cap, device=device)
-    torch.cuda.synchronize()
-    fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
-    fe.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fe.process_device(raw.data_ptr(), samples, re.data_ptr(), im.data_ptr(), cap)
-    fe.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    _, d, t = fe.ratio()
-    fe.close()
-    return {"workload": "u8 2.4 Msps -> 96 kHz, mix + 273-tap decimating FIR (D 25)", "value": round(samples / dt / 1e6, 1),
-            "unit": "Msamples/s", "ms_per_call": round(dt * 1e3, 4), "samples_per_call": samples, "decimation": d,
-            "taps": t}
-
-
+# ----------------------------------------------------------------------------- main
 def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+    argv = sys.argv[1:]
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args, argv))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    ranks = Ranks(args.dry_run)
+    torch = ranks.torch
+    if not args.dry_run:
+        torch.cuda.set_device(ranks.local)
+        # a real stream shared by torch and librfa (not the null stream)
+        torch.cuda.set_stream(torch.cuda.Stream(ranks.device))
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    n, frames, fmt, calls = args.fft_size, args.frames, args.format, args.calls_per_step
+    result = {"metric": METRIC}
+    if args.dry_run:
+        slow, per = timed(ranks, lambda k: time.sleep(0.001 * (1 + ranks.rank)), args.steps, args.warmup)
+        kernel_ms, kernel_name, span = 0.0, "dry-run", None
+        mine = frames
+    elif args.mode == "streams":
+        slow, per, kernel_ms, kernel_name = run_streams(args, ranks, fmt, args.steps, args.warmup, 3 + ranks.rank)
+        mine = frames
+    else:
+        slow, per, kernel_ms, kernel_name, span = run_shard(args, ranks, args.steps, args.warmup)
+        mine = span[1] - span[0]
 
-    import rfanalyzer_amd
-
-    n, frames, fmt = args.fft_size, args.frames, args.format
-    stream = torch.cuda.Stream(device)  # a real stream shared by torch and librfa (not the null stream)
-    torch.cuda.set_stream(stream)
-
-    def run(fmt, steps, warmup, seed, sync_ranks):
-        """Warm up, then time `steps` rfa_process() steps of one batch each (barrier +
-        synchronize on both sides).  Returns (wall seconds, main-kernel ms per launch, kernel)."""
-        eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
-                                            ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
-                                            ring_rows=args.ring_rows, device=local)
-        eng.set_stream(stream.cuda_stream)
-        pool = make_pool(torch, n, frames, fmt, args.pool_mib, seed, device)
-        eng.set_tuning(100_000_000, 20_000_000)
-
-        def step(k):
-            eng.process_tensor(pool[k % len(pool)], frames, 0, None)
-
-        for k in range(warmup):
-            step(k)
-        torch.cuda.synchronize()
-        if sync_ranks:
-            dist.barrier()
-        torch.cuda.synchronize()
-        eng.set_profiling(True)
-        ms0, l0 = eng.kernel_time()
-        t0 = time.perf_counter()
-        for k in range(steps):
-            step(warmup + k)
-        torch.cuda.synchronize()
-        if sync_ranks:
-            dist.barrier()
-        torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0
-        ms1, l1 = eng.kernel_time()
-        eng.set_profiling(False)
-        name = eng.main_kernel_name()
-        eng.close()
-        del pool
-        return elapsed, (ms1 - ms0) / max(1, l1 - l0), name
-
-    elapsed, kernel_ms, kernel_name = run(fmt, args.steps, args.warmup, 3 + rank, world > 1)
-    elapsed = max_over_ranks(elapsed, world, device)
-
-    samples = world * args.steps * frames * n
-    msps = samples / elapsed / 1e6
+    total_frames = (ranks.world if args.mode == "streams" else 1) * frames * calls * args.steps
+    samples = total_frames * n
+    msps = samples / slow / 1e6
     s_in = BPS[fmt]
-    alg_bytes = frames * n * (s_in + 4)  # per main-kernel launch: raw IQ in + one fp32 row out
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        with open(args.traffic_file) as fh:
-            tr = json.load(fh)
-        key = f"{fmt}_{n}_{frames}"
-        if key in tr:
-            traffic = tr[key]["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
-        pass
-    result = {
-        "metric": "IQ Msamples/s + waterfall lines/s at 64k FFT; achieved HBM GB/s vs roofline",
+    alg_bytes = mine * n * (s_in + 4)  # per main-kernel launch: raw IQ in + one fp32 row value out
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    result.update({
         "value": round(msps, 2),
         "unit": "Msamples/s",
-        "n_gpus": world,
+        "n_gpus": ranks.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "ms_per_step": round(slow * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.mode == "streams" else "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic",
-        "lines_per_s": round(samples / n / elapsed, 1),
-        "config": {"workload": f"config3: {n}-pt FFT, {args.window} window, {fmt} IQ, "
-                               f"{'EMA' if args.avg == 'ema' else args.avg} + "
-                               f"{'peak-hold' if not args.no_peak else 'no peak'}, ring {args.ring_rows} rows, "
-                               f"one stream per GPU",
-                   "fft_size": n, "frames_per_step": frames, "input_format": fmt, "avg": args.avg,
-                   "ema_alpha": args.ema_alpha, "peak_hold": not args.no_peak, "ring_rows": args.ring_rows,
-                   "parallelism": f"streams{world}"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                     "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
-                     "alg_bytes_per_launch": alg_bytes},
-    }
-    if rank == 0 and world == 1:
-        result["roofline"]["copy_GBps"] = copy_ceiling(torch, device)
-        result["roofline"]["frac_of_copy"] = round(achieved / result["roofline"]["copy_GBps"], 4)
-    if rank == 0 and world == 1 and fmt != "f32" and args.f32_steps > 0:
+        "data": "synthetic" if not args.dry_run else "none (dry run)",
+        "lines_per_s": round(total_frames / slow, 1),
+        "per_rank_s": [round(x, 6) for x in per],
+    })
+    if args.mode == "streams":
+        workload = (f"config3: {n}-pt FFT, {args.window} window, {fmt} IQ, "
+                    f"{'EMA' if args.avg == 'ema' else args.avg} + {'peak-hold' if not args.no_peak else 'no peak'}, "
+                    f"ring {args.ring_rows} rows, one stream per GPU")
+    else:
+        workload = (f"config4: batches of {frames} frames x {n}-pt FFT, {args.window}, {fmt} IQ, frames sharded "
+                    f"over {ranks.world} GPU(s) (contiguous ranges){', rows gathered to rank 0' if args.gather else ''}")
+    result["config"] = {"workload": workload, "fft_size": n, "frames_per_call": frames, "calls_per_step": calls,
+                        "input_format": fmt, "parallelism": f"{args.mode}{ranks.world}"}
+    if args.mode == "streams":
+        result["config"].update({"avg": args.avg, "ema_alpha": args.ema_alpha, "peak_hold": not args.no_peak,
+                                 "ring_rows": args.ring_rows})
+    result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                          "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
+                          "alg_bytes_per_launch": alg_bytes,
+                          "timing": "HIP events on the handle stream around every main-kernel launch of the timed region"}
+    single = ranks.rank == 0 and ranks.world == 1 and not args.dry_run
+    if single:
+        tr, src = pmc_traffic(args, fmt, n, frames)
+        result["roofline"]["traffic"] = tr
+        result["roofline"]["traffic_source"] = src
+        gbps, ok = copy_ceiling(torch, ranks.device)
+        result["roofline"]["copy_GBps"] = gbps
+        result["roofline"]["copy_kernel"] = "rfa_stream_copy (librfa float4 copy)" + ("" if ok else " MISMATCH")
+        result["roofline"]["frac_of_copy"] = round(achieved / gbps, 4)
+        if args.mode == "streams":
+            # step level: every byte the step must move (raw in, ring row out, EMA + peak read+write) / step time
+            step_bytes = frames * n * (s_in + 4) + 16 * n
+            result["roofline"]["step_frac"] = round(step_bytes * calls * args.steps / slow / 1e9 / HBM_PEAK_GBPS, 4)
+    if single and args.mode == "streams" and fmt != "f32" and args.f32_steps > 0:
         # BASELINE.json asks for 8-bit AND float32 IQ: the same workload on complex-float32
         # input (12 B/sample algorithmic), reported beside the headline (never `value`)
-        el32, k32, _ = run("f32", args.f32_steps, args.warmup, 103, False)
+        el32, _, k32, _ = run_streams(args, ranks, "f32", args.f32_steps, 1, 103)
         alg32 = frames * n * (BPS["f32"] + 4)
-        result["f32"] = {"value": round(args.f32_steps * frames * n / el32 / 1e6, 2), "unit": "Msamples/s",
+        result["f32"] = {"value": round(args.f32_steps * calls * frames * n / el32 / 1e6, 2), "unit": "Msamples/s",
                          "ms_per_step": round(el32 * 1e3 / args.f32_steps, 4), "kernel_ms": round(k32, 4),
                          "roofline_achieved_GBps": round(alg32 / (k32 * 1e-3) / 1e9, 1),
                          "roofline_frac": round(alg32 / (k32 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "alg_bytes_per_launch": alg32}
-    if rank == 0 and world == 1 and args.demod_steps > 0:
-        result["demod"] = demod_companion(torch, device, args.demod_steps)
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if single and args.demod_steps > 0:
+        result["demod"] = demod_companion(torch, ranks.device, args.demod_steps)
+    if ranks.rank == 0 and ranks.world == 1 and args.cpu_seconds > 0 and args.mode == "streams":
         result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds, min(16, os.cpu_count() or 1))
-    if rank == 0:
+        result["cpu_baseline"]["config1"] = config1_replay(not args.dry_run)
+    if ranks.rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.close()
 
 
 if __name__ == "__main__":

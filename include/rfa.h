@@ -217,8 +217,19 @@ RFA_API int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_
 RFA_API int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, size_t count, float *peak,
                                  float *avg);
 
-/* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers. */
+/* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers.
+ * peaks and EMA are in natural (fft-shifted) bin order.  The ring's rows are
+ * stored in the order rfa_get_ring_order reports. */
 RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);
+
+/* Storage order of the device ring rows (no reference counterpart: the JVM
+ * waterfallBuffer rows are natural order, FftProcessor.kt:222-227, and
+ * rfa_get_ring returns them so).  *residues = RS: fft-shifted bin t of a device
+ * ring row lives at element (t mod RS) * (N/RS) + t / RS.  RS = 1 is natural
+ * order; the N = 64 K / 128 K kernels compute a frame as RS residue sub-FFTs and
+ * store each residue's bins as one contiguous block (whole cache lines per
+ * workgroup).  Every rfa_* consumer of the ring handles this internally. */
+RFA_API int rfa_get_ring_order(const rfa_handle *h, int32_t *residues);
 
 /* Reference-seam entry points (host arrays, synchronous).  They use the
  * handle's N; the window/format of the handle are ignored where the reference
@@ -233,6 +244,12 @@ RFA_API int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n
 
 /* Profiling: when enabled, HIP events bracket every main FFT kernel launch on
  * the handle stream and the summed device time is reported. */
+/* Measurement support (no reference counterpart).  rfa_stream_copy: the device
+ * stream-copy kernel whose rate is the measured bandwidth ceiling SURVEY.md
+ * §8(d) asks the bench to report beside the 8 TB/s spec (float4 loads and
+ * stores, several in flight per lane; bytes a multiple of 16, 16-byte aligned
+ * device pointers), asynchronous on `stream` (a hipStream_t, NULL = default). */
+RFA_API int rfa_stream_copy(void *dst, const void *src, size_t bytes, void *stream);
 RFA_API int rfa_set_profiling(rfa_handle *h, int enable);
 RFA_API int rfa_get_kernel_time(rfa_handle *h, double *total_ms, int64_t *launches);
 /* Host-only helper (no device work): the waterfall shift in bins applied by

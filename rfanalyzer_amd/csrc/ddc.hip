@@ -634,7 +634,8 @@ int rebuild_filter(rfa_ddc *d) {
 // the initial 1 is checked once before it wraps to 0, so the first output is at
 // input 1 (FirFilter.kt:46,78,101-103; ApplicationTest.kt testFirFilter2 has 63
 // outputs for 64 inputs).
-long long out_offset(const rfa_ddc *d) { return d->mode == 0 ? (d->D >= 2 ? d->D - 1 : 1) : 0; }
+// Mode 0 (Decimator) and mode 2 (FirFilter with explicit taps) share FirFilter's counter.
+long long out_offset(const rfa_ddc *d) { return d->mode != 1 ? (d->D >= 2 ? d->D - 1 : 1) : 0; }
 
 // Outputs available once `in_total` inputs have been consumed: every n with
 // c_n < in_total (FirFilter.kt:75-98, RationalResampler.kt:80-123).
@@ -962,7 +963,8 @@ int rfa_ddc_get_stream(const rfa_ddc *d, void **stream) {
 
 int rfa_ddc_get_taps(const rfa_ddc *d, float *taps, size_t capacity, int32_t *num_taps, int32_t *decimation) {
     if (!d) return RFA_ERR_INVALID;
-    const std::vector<float> &t = d->mode == 0 ? d->taps : d->proto;   // prototype filter as designed
+    // decimator / explicit FirFilter taps as given; resampler: the prototype filter as designed
+    const std::vector<float> &t = d->mode == 1 ? d->proto : d->taps;
     if (num_taps) *num_taps = (int32_t)t.size();
     if (decimation) *decimation = d->D;
     if (taps) {

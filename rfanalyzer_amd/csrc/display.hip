@@ -49,6 +49,7 @@ __global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
     if (i >= a.width) return;
     const int buffer_index = (a.read_index + row_number) % a.ring_rows;
     const float *row = a.ring + (size_t)buffer_index * a.n;
+    const int lm = (31 - __clz(a.n)) - a.ring_logrs;  // ring storage order (ring_pos)
     unsigned *out = a.colors + (size_t)buffer_index * a.width + i;
     if (i >= a.first_pixel + 1 && i < a.last_pixel - 1) {
         const bool peaks_here = row_number == 0 && a.peaks_y;
@@ -60,7 +61,7 @@ __global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
         int j = kt_toint((float)i * a.samples_per_px);
         if (j + a.start < 0) j = -a.start;
         for (; (float)j < hi && j + a.start < a.n; j++) {
-            avg += row[j + a.start];
+            avg += row[ring_pos(j + a.start, a.ring_logrs, lm)];
             if (peaks_here) peak_avg += a.peaks[j + a.start];
             counter++;
         }
@@ -123,16 +124,17 @@ __global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
 // divided by the count, then toFloat().  One workgroup per window; the double
 // partial sums meet in LDS (a different summation order than the JVM's
 // sequential one, equal after the final rounding to float up to one ulp).
-__global__ void __launch_bounds__(256) row_window_kernel(const float *row, const int *lo, const int *hi, int count,
-                                                         float *peak, float *avg) {
+__global__ void __launch_bounds__(256) row_window_kernel(const float *row, int logrs, int n, const int *lo,
+                                                         const int *hi, int count, float *peak, float *avg) {
     const int w = blockIdx.x;
     if (w >= count) return;
+    const int lm = (31 - __clz(n)) - logrs;  // ring storage order (ring_pos)
     const int a = lo[w], b = hi[w];
     float mx = -INFINITY;
     bool nan = false;
     double s = 0.0;
     for (int j = a + (int)threadIdx.x; j <= b; j += 256) {
-        const float x = row[j];
+        const float x = row[ring_pos(j, logrs, lm)];
         nan |= x != x;
         mx = x > mx ? x : mx;
         s += (double)x;
@@ -158,10 +160,10 @@ __global__ void __launch_bounds__(256) row_window_kernel(const float *row, const
     }
 }
 
-hipError_t launch_row_windows(const float *row, const int *lo, const int *hi, int count, float *peak, float *avg,
-                              hipStream_t s) {
+hipError_t launch_row_windows(const float *row, int ring_logrs, int n, const int *lo, const int *hi, int count,
+                              float *peak, float *avg, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(row_window_kernel, dim3(count), dim3(256), 0, s, row, lo, hi, count, peak, avg);
+    hipLaunchKernelGGL(row_window_kernel, dim3(count), dim3(256), 0, s, row, ring_logrs, n, lo, hi, count, peak, avg);
     return hipGetLastError();
 }
 

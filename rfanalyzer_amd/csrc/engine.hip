@@ -51,6 +51,7 @@ struct rfa_handle {
     int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     int wide_big = 15;                // RFA_WIDE_LOGM: 15 (32 K workgroups) or 14 for N > 16 K
+    int ring_logrs = 0;               // ring row order (fft_kernels.h ring_pos): residue split of the main kernel
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
@@ -268,10 +269,14 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.variant = h->variant;
     if (a.window == h->d_window) a.window_il = h->d_window_il;
     else if (h->logn > 14) a.variant = 1;  // seam windows have no interleaved copy: narrow kernel
+    // the ring order is a property of the wide kernel's residue split (ring_pos)
+    if (a.ring && h->ring_logrs && a.variant == 1) return fail(h, RFA_ERR_INVALID, "ring order needs the wide kernel");
     a.max_logm = h->max_logm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->profile) {
-        if (h->ev_pending.size() > 256) drain_events(h, true);
+        // collect finished pairs without blocking; block (oldest first) only when far behind
+        if (h->ev_pending.size() > 512) drain_events(h, false);
+        if (h->ev_pending.size() > 4096) drain_events(h, true);
         e0 = get_event(h);
         e1 = get_event(h);
         hipEventRecord(e0, h->stream);
@@ -466,6 +471,12 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMemset(h->d_stamps, 0, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_HIP);
     }
     if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
+    // ring row order: residue-major when the wide kernel splits N into residue
+    // sub-FFTs (whole-line stores per workgroup); RFA_RING_NATURAL=1 keeps natural order
+    if (h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(logn) && logn <= 17) {
+        const char *nat = std::getenv("RFA_RING_NATURAL");
+        if (!(nat && std::atoi(nat) != 0)) h->ring_logrs = logn - rfa::wide_logm(logn, h->wide_big);
+    }
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
     h->tw_shift = (logn + 1) / 2;
@@ -664,6 +675,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_rows = h->ring_rows;
         a.ring_base = h->write_index;
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
+        a.ring_logrs = h->ring_logrs;
     }
     int rc = launch_main(h, a);
     if (rc) return rc;
@@ -682,6 +694,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             s.rows = h->d_ring;
             s.ring_rows = h->ring_rows;
             s.ring_base = h->write_index;
+            s.ring_logrs = h->ring_logrs;
         } else {
             s.rows = state_rows;
             s.row_stride = n;
@@ -768,7 +781,7 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
         if (fdiff != 0) {
             const long long off = rfa_retune_offset(fdiff, h->n, sample_rate);
             if ((off < 0 && -off < h->n) || (off >= 0 && off < h->n)) {
-                HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, (int)off, kRingFill,
+                HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, h->ring_logrs, (int)off, kRingFill,
                                                  h->stream));
                 std::swap(h->d_ring, h->d_ring_tmp);
             } else {
@@ -819,6 +832,7 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
     a.start = start;
     a.min_db = p->min_db;
     a.ring = h->d_ring;
+    a.ring_logrs = h->ring_logrs;
     a.peaks = peaks_y ? h->d_peaks : nullptr;
     a.ring_rows = R;
     a.n = n;
@@ -873,7 +887,7 @@ int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, si
     HIPCHK(h, hipMemcpyAsync(d_lo, lo, count * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(d_hi, hi, count * 4, hipMemcpyHostToDevice, h->stream));
     const float *row = h->d_ring + (size_t)h->read_index * h->n;  // FftProcessorData.readIndex: newest row
-    HIPCHK(h, rfa::launch_row_windows(row, d_lo, d_hi, (int)count, d_pk, d_av, h->stream));
+    HIPCHK(h, rfa::launch_row_windows(row, h->ring_logrs, h->n, d_lo, d_hi, (int)count, d_pk, d_av, h->stream));
     HIPCHK(h, hipMemcpyAsync(peak, d_pk, count * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipMemcpyAsync(avg, d_av, count * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -925,7 +939,8 @@ int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out) {
     if (length >= h->ring_rows) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
-    HIPCHK(h, rfa::launch_boxcar(h->d_ring, h->ring_rows, h->n, h->read_index, length, h->d_boxcar, h->stream));
+    HIPCHK(h, rfa::launch_boxcar(h->d_ring, h->ring_rows, h->n, h->ring_logrs, h->read_index, length, h->d_boxcar,
+                                  h->stream));
     HIPCHK(h, hipMemcpyAsync(out, h->d_boxcar, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
@@ -937,7 +952,12 @@ int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_
     int rc = set_device(h);
     if (rc) return rc;
     if (out) {
-        HIPCHK(h, hipMemcpyAsync(out, h->d_ring, (size_t)h->ring_rows * h->n * sizeof(float), hipMemcpyDeviceToHost,
+        const float *src = h->d_ring;
+        if (h->ring_logrs) {  // residue-major storage -> natural rows (d_ring_tmp is free outside a retune)
+            HIPCHK(h, rfa::launch_ring_natural(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, h->ring_logrs, h->stream));
+            src = h->d_ring_tmp;
+        }
+        HIPCHK(h, hipMemcpyAsync(out, src, (size_t)h->ring_rows * h->n * sizeof(float), hipMemcpyDeviceToHost,
                                  h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
@@ -993,6 +1013,12 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
     nh->profile = h->profile;
     std::swap(*h, *nh);
     rfa_destroy(nh);  // the old tables and buffers
+    return RFA_OK;
+}
+
+int rfa_get_ring_order(const rfa_handle *h, int32_t *residues) {
+    if (!h || !residues) return RFA_ERR_INVALID;
+    *residues = 1 << h->ring_logrs;
     return RFA_OK;
 }
 
@@ -1056,6 +1082,13 @@ int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n) {
     if (!h || !in || !out) return RFA_ERR_INVALID;
     if (n != (size_t)h->n) return fail(h, RFA_ERR_SIZE, "array length != fft_size");
     return single_frame(h, in, 2 * n * sizeof(float), RFA_IN_F32_INTERLEAVED, h->d_window_none, nullptr, (float2 *)out);
+}
+
+int rfa_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
+    if ((!dst || !src) && bytes) return RFA_ERR_INVALID;
+    if (bytes % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16) return RFA_ERR_INVALID;
+    if (rfa::launch_stream_copy(dst, src, bytes, (hipStream_t)stream) != hipSuccess) return RFA_ERR_HIP;
+    return RFA_OK;
 }
 
 int rfa_set_profiling(rfa_handle *h, int enable) {

@@ -332,11 +332,34 @@ __device__ __forceinline__ typename Raw<FMT>::T load_raw(const uint8_t *fb, int 
 // LUTs: s8 b/128 (Signed8BitIQConverter.java:48-50), u8 (b-127.4f)/128
 // (Unsigned8BitIQConverter.java:48-50), s16 s/32768 (Signed16BitIQConverter.kt:52-55);
 // scaling by a power of two commutes with the fp32 rounding of the window multiply.
+// Signed byte / word field of a dword -> float in ONE instruction: SDWA operand
+// select with sign extension (hipcc emits a bfe/ashr + convert pair per value).
+template <int SEL>  // 0, 1: BYTE_0 / BYTE_1; 4, 5: WORD_0 / WORD_1
+__device__ __forceinline__ float cvt_sext(unsigned v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    float r;
+    if constexpr (SEL == 0)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0" : "=v"(r) : "v"(v));
+    else if constexpr (SEL == 1)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(r) : "v"(v));
+    else if constexpr (SEL == 4)
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0" : "=v"(r) : "v"(v));
+    else
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1" : "=v"(r) : "v"(v));
+    return r;
+#else
+    if constexpr (SEL == 0) return (float)(signed char)(v & 0xff);
+    else if constexpr (SEL == 1) return (float)(signed char)((v >> 8) & 0xff);
+    else if constexpr (SEL == 4) return (float)(short)(v & 0xffff);
+    else return (float)(short)(v >> 16);
+#endif
+}
+
 template <int FMT>
 __device__ __forceinline__ float2 convert_raw(typename Raw<FMT>::T v) {
-    if constexpr (FMT == 0) return make_float2((float)(signed char)(v & 0xff), (float)(signed char)(v >> 8));
+    if constexpr (FMT == 0) return make_float2(cvt_sext<0>(v), cvt_sext<1>(v));
     else if constexpr (FMT == 1) return make_float2((float)(v & 0xff) - 127.4f, (float)(v >> 8) - 127.4f);
-    else if constexpr (FMT == 2) return make_float2((float)(short)(v & 0xffff), (float)(short)(v >> 16));
+    else if constexpr (FMT == 2) return make_float2(cvt_sext<4>(v), cvt_sext<5>(v));
     else return v;
 }
 

@@ -9,6 +9,17 @@
 
 namespace rfa {
 
+// Ring row storage order.  When the main kernel computes an N-point
+// frame as RS = 2^logrs residue sub-FFTs of M = N/RS points (the wide kernel at
+// N = 64 K / 128 K), residue r's bins are stored as one contiguous block: the
+// fft-shifted bin t of a ring row lives at element (t mod RS)*M + t/RS, so every
+// residue workgroup writes whole cache lines.  logrs = 0 is natural order.  Only
+// the device ring uses this order; caller rows, peaks, EMA and every host copy
+// are in natural order (ring consumers gather through ring_pos).
+__host__ __device__ __forceinline__ int ring_pos(int t, int logrs, int logm) {
+    return ((t & ((1 << logrs) - 1)) << logm) | (t >> logrs);
+}
+
 // Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
 // 128 KiB + padding, one workgroup per CU).  Larger N split across
 // workgroups (see DESIGN.md "Large N").
@@ -37,6 +48,7 @@ struct FftLaunch {
     int ring_rows = 0;
     int ring_base = 0;          // ring row of frame 0 (reference writeIndex)
     int ring_first = 0;         // first frame that is stored into the ring
+    int ring_logrs = 0;         // ring row order (ring_pos); must equal the kernel's residue split or 0
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
     // decimation in time for N > 2^17 (wide kernel, complex out): with dit_ss = S > 1
     // work item u is sub-frame (frame u / S, residue u % S) = samples S*m + u % S of a
@@ -98,6 +110,7 @@ struct StateLaunch {
     long long row_stride = 0;
     int ring_rows = 0;
     int ring_base = 0;
+    int ring_logrs = 0;      // ring row order (ring_pos), ring mode only
     int n_frames = 0;
     int n = 0;
     float *peaks = nullptr;  // may be null
@@ -118,6 +131,7 @@ struct DrawLaunch {
     const float *ring = nullptr;   // [ring_rows][n]
     const float *peaks = nullptr;  // [n] or null
     int ring_rows = 0, n = 0, read_index = 0;
+    int ring_logrs = 0;            // ring row order (ring_pos)
     int width = 0, fft_height = 0, avg_length = 0;
     int start = 0, first_pixel = 0, last_pixel = 0;
     float samples_per_px = 0.f, min_db = 0.f, db_width = 0.f, scale = 0.f;
@@ -132,16 +146,23 @@ struct DrawLaunch {
 };
 hipError_t launch_draw(const DrawLaunch &a);
 // Peak / mean of inclusive bin windows of one row (scanner reductions), display.hip.
-hipError_t launch_row_windows(const float *row, const int *lo, const int *hi, int count, float *peak, float *avg,
-                              hipStream_t s);
+hipError_t launch_row_windows(const float *row, int ring_logrs, int n, const int *lo, const int *hi, int count,
+                              float *peak, float *avg, hipStream_t s);
 
 // Ring maintenance (FftProcessor.kt:197-220) and boxcar (AnalyzerSurface.kt:710-714).
 hipError_t launch_fill(float *p, long long count, float value, hipStream_t s);
-hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s);
-hipError_t launch_boxcar(const float *ring, int rows, int n, int read_index, int length, float *out, hipStream_t s);
+hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int logrs, int shift, float fill,
+                             hipStream_t s);
+hipError_t launch_boxcar(const float *ring, int rows, int n, int logrs, int read_index, int length, float *out,
+                         hipStream_t s);
+// Ring rows in natural order (host read-back): dst[row][t] = src[row][ring_pos(t)].
+hipError_t launch_ring_natural(const float *src, float *dst, int rows, int n, int logrs, hipStream_t s);
 // Waterfall-speed resize (FftProcessor.kt:185-195): dst[i] = src[(write_index + i) % src_rows]
 // for i < src_rows, fill beyond; dst has dst_rows rows.
 hipError_t launch_ring_rotate(const float *src, int src_rows, float *dst, int dst_rows, int n, int write_index,
                               float fill, hipStream_t s);
+
+// Streaming float4 copy (bench copy ceiling, rfa_stream_copy).
+hipError_t launch_stream_copy(void *dst, const void *src, size_t bytes, hipStream_t s);
 
 }  // namespace rfa

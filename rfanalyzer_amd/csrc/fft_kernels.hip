@@ -396,6 +396,23 @@ __device__ __forceinline__ const float *state_row(const StateLaunch &a, int f) {
     }
     return a.rows + (size_t)((long long)f * a.row_stride);
 }
+// ring_pos order of the rows the state kernels read (the ring's; caller rows are natural)
+__device__ __forceinline__ int state_logrs(const StateLaunch &a) { return a.ring_rows > 0 ? a.ring_logrs : 0; }
+__device__ __forceinline__ int ilog2_dev(int n) { return 31 - __clz(n); }
+
+// Fft-shifted bins [t, t+4) of a row (t a multiple of 4): one 16-B load in natural
+// order; in the residue-major ring (ring_pos) two 8-B loads for RS = 2 (bins t, t+2
+// in residue 0's block, t+1, t+3 in residue 1's) or a gather for RS = 4.
+__device__ __forceinline__ float4 load_bins4(const float *row, int t, int logrs, int logm) {
+    if (logrs == 0) return *reinterpret_cast<const float4 *>(row + t);
+    if (logrs == 1) {
+        const float2 a0 = *reinterpret_cast<const float2 *>(row + (t >> 1));
+        const float2 a1 = *reinterpret_cast<const float2 *>(row + (1 << logm) + (t >> 1));
+        return make_float4(a0.x, a1.x, a0.y, a1.y);
+    }
+    return make_float4(row[ring_pos(t, logrs, logm)], row[ring_pos(t + 1, logrs, logm)],
+                       row[ring_pos(t + 2, logrs, logm)], row[ring_pos(t + 3, logrs, logm)]);
+}
 
 // Sequential peak-hold / EMA over the batch (one thread per bin, frames in order).
 // Peak: FftProcessor.kt:229-232.  EMA (extension): em += alpha (x - em); an
@@ -406,9 +423,10 @@ __global__ void state_kernel(StateLaunch a) {
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     const float al = a.ema_alpha;
+    const int lr = state_logrs(a), pos = ring_pos(bin, lr, ilog2_dev(a.n) - lr);
 #pragma unroll 8
     for (int f = 0; f < a.n_frames; f++) {
-        const float x = state_row(a, f)[bin];
+        const float x = state_row(a, f)[pos];
         pk = fmaxf(pk, x);
         em = (em > -INFINITY) ? em + al * (x - em) : x;
     }
@@ -430,6 +448,7 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
     if (bin >= a.n) return;
     const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
     const float al = a.ema_alpha, keep = 1.0f - al;
+    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float pk[4], emi[4], b[4];
     bool restart[4];
 #pragma unroll
@@ -437,7 +456,7 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
     float am = 1.0f;
 #pragma unroll 4
     for (int f = f0; f < f1; f++) {
-        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);
+        const float4 x4 = load_bins4(state_row(a, f), bin, lr, lm);
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -480,6 +499,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     const int bin = blockIdx.x * BPB + 4 * l;
     const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
     const float al = a.ema_alpha, keep = 1.0f - al;
+    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float pk[4], emi[4], b[4];
     bool restart[4];
 #pragma unroll
@@ -487,7 +507,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     float am = 1.0f;
 #pragma unroll 4
     for (int f = f0; f < f1; f++) {
-        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);
+        const float4 x4 = load_bins4(state_row(a, f), bin, lr, lm);
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -548,8 +568,9 @@ hipError_t launch_state(const StateLaunch &a) {
 __global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int first, int last, float *out) {
     const int f = blockIdx.x;
     const float *row = state_row(a, f);
+    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float s = 0.0f;
-    for (int i = first + (int)threadIdx.x; i < last; i += 256) s += row[i];
+    for (int i = first + (int)threadIdx.x; i < last; i += 256) s += row[ring_pos(i, lr, lm)];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     __shared__ float part[4];
@@ -578,20 +599,39 @@ hipError_t launch_fill(float *p, long long count, float value, hipStream_t s) {
     return hipGetLastError();
 }
 
-// dst[row][i] = src[row][i - shift] (fill outside) -- FftProcessor.kt:202-209
-__global__ void ring_shift_kernel(const float *src, float *dst, int n, int shift, float fill) {
+// dst[row][i] = src[row][i - shift] (fill outside) -- FftProcessor.kt:202-209; bins
+// i addressed through the ring's storage order (ring_pos)
+__global__ void ring_shift_kernel(const float *src, float *dst, int n, int logrs, int shift, float fill) {
     const int row = blockIdx.y;
+    const int lm = ilog2_dev(n) - logrs;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int s = i - shift;
-        dst[(size_t)row * n + i] = (s >= 0 && s < n) ? src[(size_t)row * n + s] : fill;
+        dst[(size_t)row * n + ring_pos(i, logrs, lm)] =
+            (s >= 0 && s < n) ? src[(size_t)row * n + ring_pos(s, logrs, lm)] : fill;
     }
 }
 
-hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int shift, float fill, hipStream_t s) {
+hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int logrs, int shift, float fill,
+                             hipStream_t s) {
     if (rows <= 0) return hipSuccess;
     int bx = (n + 255) / 256;
     if (bx > 64) bx = 64;
-    hipLaunchKernelGGL(ring_shift_kernel, dim3(bx, rows), dim3(256), 0, s, src, dst, n, shift, fill);
+    hipLaunchKernelGGL(ring_shift_kernel, dim3(bx, rows), dim3(256), 0, s, src, dst, n, logrs, shift, fill);
+    return hipGetLastError();
+}
+
+__global__ void ring_natural_kernel(const float *src, float *dst, int n, int logrs) {
+    const int row = blockIdx.y;
+    const int lm = ilog2_dev(n) - logrs;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        dst[(size_t)row * n + i] = src[(size_t)row * n + ring_pos(i, logrs, lm)];
+}
+
+hipError_t launch_ring_natural(const float *src, float *dst, int rows, int n, int logrs, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    int bx = (n + 255) / 256;
+    if (bx > 64) bx = 64;
+    hipLaunchKernelGGL(ring_natural_kernel, dim3(bx, rows), dim3(256), 0, s, src, dst, n, logrs);
     return hipGetLastError();
 }
 
@@ -618,17 +658,48 @@ hipError_t launch_ring_rotate(const float *src, int src_rows, float *dst, int ds
 }
 
 // AnalyzerSurface.kt:710-714 at bin resolution: fp32 sum newest-first, / (L+1).
-__global__ void boxcar_kernel(const float *ring, int rows, int n, int read_index, int length, float *out) {
+__global__ void boxcar_kernel(const float *ring, int rows, int n, int logrs, int read_index, int length, float *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const int p = ring_pos(i, logrs, ilog2_dev(n) - logrs);
     float acc = 0.f;
-    for (int r = 0; r <= length; r++) acc += ring[(size_t)((read_index + r) % rows) * n + i];
+    for (int r = 0; r <= length; r++) acc += ring[(size_t)((read_index + r) % rows) * n + p];
     out[i] = acc / (float)(length + 1);
 }
 
-hipError_t launch_boxcar(const float *ring, int rows, int n, int read_index, int length, float *out,
+hipError_t launch_boxcar(const float *ring, int rows, int n, int logrs, int read_index, int length, float *out,
                          hipStream_t s) {
-    hipLaunchKernelGGL(boxcar_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ring, rows, n, read_index, length, out);
+    hipLaunchKernelGGL(boxcar_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ring, rows, n, logrs, read_index,
+                       length, out);
+    return hipGetLastError();
+}
+
+// Streaming copy at the HBM ceiling (bench denominator): 4 float4 per lane in
+// flight, grid-stride over 16-KiB blocks per workgroup iteration.
+__global__ void __launch_bounds__(256) stream_copy_kernel(float4 *__restrict__ dst, const float4 *__restrict__ src,
+                                                          long long n4) {
+    constexpr int U = 4;
+    const long long stride = (long long)gridDim.x * 256 * U;
+    for (long long base = (long long)blockIdx.x * 256 * U + threadIdx.x; base < n4; base += stride) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (base + u * 256 < n4) v[u] = src[base + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (base + u * 256 < n4) dst[base + u * 256] = v[u];
+    }
+}
+
+hipError_t launch_stream_copy(void *dst, const void *src, size_t bytes, hipStream_t s) {
+    const long long n4 = (long long)(bytes / 16);
+    if (n4 <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const long long blocks = std::min<long long>((n4 + 1023) / 1024, (long long)cus * 8);
+    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<float4 *>(dst),
+                       static_cast<const float4 *>(src), n4);
     return hipGetLastError();
 }
 

@@ -1,14 +1,13 @@
-// gfx950 "wide" sub-FFT kernel for M = 8192 / 16384: 256 threads, 64 points
-// per thread, two workgroups per CU.
+// gfx950 "wide" sub-FFT kernel: one M-point sub-FFT (M = 8192, 16384 or 32768)
+// per work item, 32 points per thread in VGPRs, M/32 threads per workgroup (256
+// for 8 K, 512 for 16 K, 1024 for 32 K).
 //
-// Why this shape (measured, DESIGN.md "Kernel design"): with one 1024-thread
-// workgroup per CU every wave runs the same phase between barriers, so HBM
-// loads, VALU butterflies, LDS exchanges and row stores never overlap and the
-// kernel time is their SUM.  Here each thread keeps 64 points in VGPRs
-// (256-VGPR budget at 2 waves/SIMD), an M-point FFT needs only two LDS
-// exchanges (radix 32,32,16 for 16K; 32,16,16 for 8K), and each exchange runs
-// in two half-rounds through an M/2 buffer, so a workgroup needs ~66 KiB of
-// LDS and two of them share a CU and interleave their phases.
+// Shape (measured): 32 points per thread keeps the
+// kernel at 128 VGPRs (4 waves per SIMD), an M-point FFT needs three in-register
+// radix-32/16 passes and two LDS exchanges, and each exchange runs in two
+// half-rounds through an M/2 buffer (66 KiB for 16 K: two workgroups per CU;
+// 132 KiB for 32 K: one).  N = 64 K / 128 K run as RS = 2 / 4 residue work
+// items of the 32 K workgroup (decimation-in-frequency pre-stage below).
 //
 // Per work item (frame, residue r) the pipeline is the same as the narrow
 // kernel (fft_kernels.hip): raw IQ -> LUT-exact convert -> window (fp32
@@ -396,7 +395,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
-    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~112) == 0 &&
+    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~48) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
@@ -577,14 +576,16 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 rr = (a.ring_base - frame) % a.ring_rows;
                 if (rr < 0) rr += a.ring_rows;
             }
+            // ring in residue-major order (ring_pos, fft_kernels.h) when the engine asks for
+            // it: residue r's M bins are one contiguous block, so this workgroup's stores
+            // cover whole lines; caller rows are always natural (fft-shifted) order
+            const bool rm = RS > 1 && a.ring_logrs > 0;
             const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
-            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n : nullptr, to_ring ? n * 4 : 0);
-            // DIAG & 64 (profiling only): residue-major layout [r][i] instead of the
-            // interleaved bins -- same bytes, whole lines per workgroup (measures the
-            // cost of the partial-line stores)
-            const int vo = (DIAG & 64) ? tid * 4 : (RS * tid + r) * 4;
+            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n + (rm ? (size_t)r * M : 0) : nullptr,
+                                             to_ring ? (rm ? M : n) * 4 : 0);
+            const int vo = (RS * tid + r) * 4;
             // one uniform branch per item, not per store
-            auto epilogue = [&](rsrc_t rs0, rsrc_t rs1, auto both) {
+            auto epilogue = [&](auto nat_c, auto ring_c, auto rm_c) {
     #pragma unroll
                 for (int b = 0; b < PT / G::R2; b++) {
     #pragma unroll
@@ -592,21 +593,41 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                         const float2 x = v[b * G::R2 + t];
                         const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
                         // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
-                        const int so = (DIAG & 64) ? (r * M + G::TPF * b + t * (M / G::R2)) * 4
-                                                   : ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
+                        const int so = ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
+                        // residue-major: sub-bin i = tid + TPF b + t M/R2 at (i + M/2) mod M of the block
+                        const int so_rm = ((G::TPF * b + t * (M / G::R2) + M / 2) & (M - 1)) * 4;
                         if constexpr (DIAG & 2) {
                             asm volatile("" ::"v"(db));
                         } else {
-                            buf_store_f32(db, rs0, vo, so);
-                            if constexpr (decltype(both)::value) buf_store_f32(db, rs1, vo, so);
+                            if constexpr (decltype(nat_c)::value) buf_store_f32(db, row_rs, vo, so);
+                            if constexpr (decltype(ring_c)::value) {
+                                if constexpr (decltype(rm_c)::value) buf_store_f32(db, ring_rs, tid * 4, so_rm);
+                                else buf_store_f32(db, ring_rs, vo, so);
+                            }
                         }
                     }
                 }
             };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
             pending_st = (a.rows ? PT : 0) + (to_ring ? PT : 0);
-            if (a.rows && to_ring) epilogue(row_rs, ring_rs, std::true_type{});
-            else if (a.rows) epilogue(row_rs, row_rs, std::false_type{});
-            else if (to_ring) epilogue(ring_rs, ring_rs, std::false_type{});
+            if (a.rows && to_ring) {
+                if constexpr (RS > 1) {
+                    if (rm) epilogue(T_{}, T_{}, T_{});
+                    else epilogue(T_{}, T_{}, F_{});
+                } else {
+                    epilogue(T_{}, T_{}, F_{});
+                }
+            } else if (a.rows) {
+                epilogue(T_{}, F_{}, F_{});
+            } else if (to_ring) {
+                if constexpr (RS > 1) {
+                    if (rm) epilogue(F_{}, T_{}, T_{});
+                    else epilogue(F_{}, T_{}, F_{});
+                } else {
+                    epilogue(F_{}, T_{}, F_{});
+                }
+            }
             stamp(u, 6);
         }
     };
@@ -732,10 +753,6 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
     if (a.diag == 16 && a.logn == 16) {  // staged 64 K kernel without window loads (profiling only)
         if (a.fmt != 0 || co) return hipErrorInvalidValue;
         return launch_wide_one<15, 32, 2, 0, false, 16, true>(a);
-    }
-    if (a.diag == 64) {  // residue-major output layout (profiling only)
-        if (a.fmt != 0 || co || a.logn != 16) return hipErrorInvalidValue;
-        return launch_wide_one<15, 32, 2, 0, false, 64, true>(a);
     }
     if (a.diag == 32) {  // phase stamps of the staged s8 kernels (profiling only)
         if (a.fmt != 0 || co || !a.stamps) return hipErrorInvalidValue;

@@ -154,6 +154,14 @@ class SpectrumEngine:
                     "rfa_get_ring")
         return out, ri.value, wi.value
 
+    @property
+    def ring_order(self) -> int:
+        """Residues RS of the device ring's storage order (rfa_get_ring_order); ``ring()``
+        always returns natural rows."""
+        rs = ctypes.c_int32()
+        self._check(_lib.lib().rfa_get_ring_order(self._h, ctypes.byref(rs)), "rfa_get_ring_order")
+        return rs.value
+
     def reset_state(self) -> None:
         self._check(_lib.lib().rfa_reset_state(self._h), "rfa_reset_state")
 

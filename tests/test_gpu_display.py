@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 N, R, F0, SR = 2048, 12, 100_000_000, 2_000_000
 
 
-def _engine(rfa, frames):
-    e = rfa.SpectrumEngine(N, "blackman", "s8", avg="none", peak_hold=True, ring_rows=R)
+def _engine(rfa, frames, n=N):
+    e = rfa.SpectrumEngine(n, "blackman", "s8", avg="none", peak_hold=True, ring_rows=R)
     e.set_tuning(F0, SR)
-    data = signals.frames_bytes(N, frames, "s8", seed=21, tones=((0.13, 0.4), (0.31, 0.02)), noise=0.03)
+    data = signals.frames_bytes(n, frames, "s8", seed=21, tones=((0.13, 0.4), (0.31, 0.02)), noise=0.03)
     e.process(data, frames, rows=False)
     return e
 
@@ -56,6 +56,19 @@ def test_partial_ring_and_no_average(rfa):
     try:
         _assert_same(*_both(e, average_length=0, width=1000))
         _assert_same(*_both(e, average_length=R - 1, min_db=-150.0, max_db=0.0))
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("n", [65536, 131072])
+def test_residue_major_ring_bit_exact(rfa, n):
+    """At 64 K / 128 K the device ring is stored residue-major (rfa_get_ring_order);
+    the draw kernel gathers each pixel's bins in bin order, so the result is still
+    bit-identical to the restatement on the natural rows."""
+    e = _engine(rfa, 14, n)
+    try:
+        assert e.ring_order == n // 32768
+        _assert_same(*_both(e, width=1111, viewport_frequency=F0 + 150_000, viewport_sample_rate=SR // 3))
     finally:
         e.close()
 

@@ -47,6 +47,23 @@ def test_window_stats_vs_kotlin(eng):
     assert _close(av, eav)
 
 
+@pytest.mark.parametrize("n", [65536, 131072])
+def test_window_stats_on_residue_major_ring(rfa, n):
+    """The 64 K / 128 K ring is stored residue-major; the window kernel reads bins through ring_pos."""
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=3) as e:
+        e.set_tuning(F0, SR)
+        e.process(signals.frames_bytes(n, 4, "s8", seed=35, tones=((0.21, 0.3), (-0.2, 0.002)), noise=0.01), 4,
+                  rows=False)
+        row = _newest_row(e)
+        rng = np.random.default_rng(5)
+        lo = rng.integers(0, n - 1, 200).astype(np.int32)
+        hi = np.minimum(n - 1, lo + rng.integers(0, 3000, 200)).astype(np.int32)
+        pk, av = e.row_window_stats(lo, hi)
+        epk, eav = osc.window_stats(row, lo, hi)
+        np.testing.assert_array_equal(pk, epk)
+        assert _close(av, eav)
+
+
 def test_scanner_functions_match_restatement(eng):
     row = _newest_row(eng)
     # whole-row squelch level and detectSignal

@@ -71,13 +71,17 @@ def test_ring_indices_and_rows_match_processor_restatement(rfa):
     e.close()
 
 
+@pytest.mark.parametrize("n", [256, 65536, 131072])
 @pytest.mark.parametrize("new_freq,new_sr", [(100 + 37, 1000), (100 - 300, 1000), (100 + 999, 1000), (100, 2000)])
-def test_retune_shift_and_clear(rfa, new_freq, new_sr):
-    n, rows_r = 256, 4
+def test_retune_shift_and_clear(rfa, n, new_freq, new_sr):
+    """FftProcessor.kt:197-220 shift / clear; at 64 K and 128 K the device ring is stored
+    residue-major (rfa_get_ring_order 2 / 4) and the shift runs in that order."""
+    rows_r = 4
     data = np.random.default_rng(4).integers(-128, 128, size=2 * n * 3, dtype=np.int8).tobytes()
     ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, 3, None, oracle.WIN_BLACKMAN)
     p = processor.FftProcessorRef(n, rows_r, peak_hold=True)
     e = rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=rows_r)
+    assert e.ring_order == {65536: 2, 131072: 4}.get(n, 1)
     e.set_tuning(100, 1000)
     e.process(data[: 2 * 2 * n], 2, rows=False)
     p.push(ref_rows[0], 100, 1000)
@@ -94,6 +98,22 @@ def test_retune_shift_and_clear(rfa, new_freq, new_sr):
             assert gu.db_diff(ring[r][~fill], p.ring[r][~fill]) <= gu.DB_TOL
     assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL  # peaks reset on retune
     e.close()
+
+
+@pytest.mark.parametrize("n", [65536, 131072])
+def test_boxcar_over_residue_major_ring(rfa, n):
+    """rfa_get_boxcar (AnalyzerSurface.kt:710-714 at bin level) gathers the bins of the
+    residue-major ring rows back into natural order."""
+    frames, rows_r, L = 6, 5, 3
+    data = np.random.default_rng(14).integers(-128, 128, size=2 * n * frames, dtype=np.int8).tobytes()
+    ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, frames, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(n, rows_r)
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="boxcar", avg_length=L, ring_rows=rows_r) as e:
+        e.set_tuning(100, 1000)
+        e.process(data, frames, rows=False)
+        for r in ref_rows:
+            p.push(r, 100, 1000)
+        assert gu.db_diff(e.boxcar(L), p.boxcar(L)) <= gu.DB_TOL
 
 
 def test_ema_matches_sequential_extension(rfa):
@@ -141,7 +161,9 @@ def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
     data = signals.frames_bytes(n, frames, "s8", 17, tones=((0.01, 0.3), (-0.2, 0.05)), noise=0.05)
     ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, frames, None, oracle.WIN_BLACKMAN)
     exp = [processor.channel_mean(r, n, freq, sr, *chan) for r in ref_rows]
-    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=8) as e:
+    # 64 K: the batch fits the ring, so the means read the residue-major ring rows;
+    # the other sizes read the staging rows (batch larger than the ring)
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=12 if n == 65536 else 8) as e:
         e.set_tuning(freq, sr)
         e.set_channel(*chan)
         e.process(data, frames, rows=False)
