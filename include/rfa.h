@@ -308,6 +308,7 @@ RFA_API int rfa_ddc_create_fir(int device, int input_format, int32_t sample_rate
  * stream).  Pending work of the previous stream is drained first. */
 RFA_API int rfa_ddc_set_stream(rfa_ddc *d, void *stream);
 RFA_API int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimation, int32_t *taps_per_output);
+RFA_API int rfa_ddc_get_format(const rfa_ddc *d, int32_t *input_format);  /* rfa_input_format of the handle */
 RFA_API int rfa_ddc_destroy(rfa_ddc *d);
 RFA_API const char *rfa_ddc_last_error(const rfa_ddc *d);
 /* Like IQConverter.setSampleRate + the Decimator's rebuild check: the mixer

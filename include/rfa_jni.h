@@ -20,8 +20,24 @@
  *        straight to log-mag rows: the converter LUT (fillPacketIntoSamplePacket,
  *        IQSourceInterface.java:159) is fused into the same kernel.
  *
+ * Stateful natives (one jlong handle = one rfa_handle / rfa_ddc):
+ *   createAnalyzerNative / destroyAnalyzerNative / processPacketNative
+ *        FftProcessor's ring, peak-hold and averaging on the device
+ *        (FftProcessor.kt:96-257, Scheduler.kt:252-279): rfa_create, rfa_set_tuning
+ *        + rfa_process_host
+ *   drawPreprocessNative   AnalyzerSurface.drawPreprocessing (AnalyzerSurface.kt:599-743):
+ *        rfa_draw_preprocess, colours in the reference's colorBuffer layout
+ *   rowWindowStatsNative   the scanner / squelch row reductions
+ *        (MainViewModel.kt:861-929, :1391-1540): rfa_row_window_stats
+ *   ddcCreate / ddcDestroy / ddcSetFrequencies / ddcProcess
+ *        IQConverter.mixPacketIntoSamplePacket + Decimator / Resampler
+ *        (Scheduler.kt:237-250, Decimator.java:175-191): rfa_ddc_*
+ *   Handle-taking natives return an rfa_status (0 = ok, < 0 = error) or a count
+ *   (>= 0) / negative status; create functions return 0 on failure.
+ *
  * Threading: like the reference (NativeDsp.kt:23-26) one caller thread per
- * library is expected; the shim additionally serialises calls with a mutex.
+ * library is expected; the shim additionally serialises the legacy (global
+ * setup) calls with a mutex.  A handle must not be used from two threads at once.
  */
 #ifndef RFA_JNI_H
 #define RFA_JNI_H
@@ -44,6 +60,39 @@ JNIEXPORT jboolean JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performWindowe
 JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processIqBytesNative(
     JNIEnv *env, jobject thiz, jbyteArray packet, jint format, jint fft_size, jint frame_stride,
     jfloatArray mag_out);
+
+/* FftProcessor on the device.  window: rfa_window; avg_mode: rfa_avg_mode. */
+JNIEXPORT jlong JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_createAnalyzerNative(
+    JNIEnv *env, jobject thiz, jint fft_size, jint input_format, jint window, jint avg_mode, jint avg_length,
+    jfloat ema_alpha, jboolean peak_hold, jint ring_rows, jint device);
+JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_destroyAnalyzerNative(JNIEnv *env, jobject thiz,
+                                                                                     jlong handle);
+/* One raw packet (frames at frame_stride bytes, 0 = dense) into ring + state after
+ * SamplePacket.frequency / sampleRate (rfa_set_tuning).  Returns frames or < 0. */
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processPacketNative(
+    JNIEnv *env, jobject thiz, jlong handle, jbyteArray packet, jint frame_stride, jlong frequency,
+    jlong sample_rate);
+/* colorBuffer holds ringRows*width ARGB ints (colorBuffer[bufferIndex*width + i]);
+ * peaksY may be null; autoscale holds 2 floats (min, max).  Returns rfa_status. */
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_drawPreprocessNative(
+    JNIEnv *env, jobject thiz, jlong handle, jint width, jint fft_height, jlong viewport_frequency,
+    jlong viewport_sample_rate, jfloat min_db, jfloat max_db, jint average_length, jintArray color_map,
+    jintArray color_buffer, jfloatArray fft_path_y, jfloatArray peaks_y, jfloatArray autoscale);
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_rowWindowStatsNative(
+    JNIEnv *env, jobject thiz, jlong handle, jintArray lo, jintArray hi, jfloatArray peak, jfloatArray avg);
+/* Demod front end, one handle per channel; resampler: JNI_TRUE = Resampler.kt mode. */
+JNIEXPORT jlong JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcCreate(JNIEnv *env, jobject thiz, jint input_format,
+                                                                         jint sample_rate, jint output_rate,
+                                                                         jboolean resampler, jint device);
+JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcDestroy(JNIEnv *env, jobject thiz, jlong handle);
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcSetFrequencies(JNIEnv *env, jobject thiz,
+                                                                                jlong handle, jlong frequency,
+                                                                                jlong channel_frequency);
+/* Raw packet in (format of the handle), decimated planar samples out; returns the
+ * count written (SamplePacket.size) or < 0 (e.g. RFA_ERR_SIZE: re/im too short). */
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcProcess(JNIEnv *env, jobject thiz, jlong handle,
+                                                                         jbyteArray packet, jfloatArray re,
+                                                                         jfloatArray im);
 
 #ifdef __cplusplus
 }

@@ -768,6 +768,12 @@ int rfa_ddc_get_ratio(const rfa_ddc *d, int32_t *interpolation, int32_t *decimat
     return RFA_OK;
 }
 
+int rfa_ddc_get_format(const rfa_ddc *d, int32_t *input_format) {
+    if (!d || !input_format) return RFA_ERR_INVALID;
+    *input_format = d->fmt;
+    return RFA_OK;
+}
+
 int rfa_resampler_design(int32_t output_rate, int32_t input_rate, int32_t max_denominator, float fractional_bw,
                          int32_t max_taps, int32_t *interpolation, int32_t *decimation, float *taps, size_t capacity,
                          int32_t *num_taps) {

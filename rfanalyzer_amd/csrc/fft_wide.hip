@@ -208,9 +208,17 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #define PRE_DIST 1
 #endif
 
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false>
+// WP > 0 (RS = 2): the window pairs (w[m], w[m+M]) of the thread's first WP points
+// arrive preloaded in wpre[idx] (issued by the previous item's tail, see
+// fft_wide_kernel); the rest are loaded here, behind the preloaded chunks' work.
+#ifndef RFA_WPRE
+#define RFA_WPRE 0  // measured slower at 8/16/32 (profiles/r02/window_preload_ab.txt): spills
+#endif
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
-                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
+                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
+                                         const float2 *wpre = nullptr) {
+    static_assert(WP == 0 || RS == 2, "preloaded window pairs: RS = 2 only");
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));  // bytes per sample (per plane)
@@ -250,6 +258,9 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             if constexpr (NOWIN) {  // ablation (RFA_DIAG=16): constant window, no window loads
 #pragma unroll
                 for (int j = 0; j < RS; j++) win[s][q][j] = 1.0f / 128.0f;
+            } else if (WP > 0 && c * C + q < WP) {
+                win[s][q][0] = wpre[idx < WP ? idx : 0].x;
+                win[s][q][1] = wpre[idx < WP ? idx : 0].y;
             } else if constexpr (RS == 2) {
                 const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
                 win[s][q][0] = w.x;
@@ -391,7 +402,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int tid = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::HALFP;
 
-    const int work = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
+    // decimation in time: items grouped 8 frames x S residues (see body()), frames padded to 8
+    const bool dit = RS == 1 && COMPLEX_OUT && a.dit_ss > 1;
+    const int work = dit ? ((a.n_frames + 7) / 8) * 8 * a.dit_ss : a.n_frames;
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
@@ -454,6 +467,20 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // staged frame skips them -- vmcnt counts in issue order and they are younger
     // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
     int pending_st = 0;
+    // RS = 2, staged 8/16-bit input: the thread's window pairs are the same for every
+    // item; they are (re)loaded at the tail of each item, after the epilogue has
+    // freed the point registers, so the loads fly during the staged-frame wait
+    constexpr int WP = (STG && RS == 2 && !COMPLEX_OUT && (DIAG & 16) == 0) ? RFA_WPRE : 0;
+    float2 wpre[WP > 0 ? WP : 1];
+    auto load_wpre = [&]() {
+        if constexpr (WP > 0) {
+            const rsrc_t w_rs = make_rsrc(a.window_il, M * RS * 4);
+#pragma unroll
+            for (int idx = 0; idx < WP; idx++)
+                wpre[idx] = buf_load_f32x2(w_rs, tid * 8, (G::TPF * (idx >> 5) + (M / 32) * (idx & 31)) * 8);
+        }
+    };
+    load_wpre();
     auto body = [&](int u, int &unext) {
         stamp(u, 0);
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
@@ -466,9 +493,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (RS == 1) {
             frame = u * G::SLOTS + slot;
             r = 0;
-            if (COMPLEX_OUT && a.dit_ss > 1) {
-                dit_r = frame % a.dit_ss;
-                frame /= a.dit_ss;
+            if (dit) {
+                // the S residues (strided sub-frames) of a frame on one XCD (blocks b, b+8,
+                // ... share one), dispatched together: each XCD fetches a frame's lines
+                // once into its L2 and its S workgroups share them (speed only)
+                const int g = u / (8 * a.dit_ss), rem = u - g * (8 * a.dit_ss);
+                dit_r = rem >> 3;
+                frame = g * 8 + (rem & 7);
             }
         } else {
             // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
@@ -493,8 +524,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (STG) {
             // this item's frame, staged by LDS-DMA during the previous item: wait for
             // this wave's pieces, then for every wave's (the barrier)
-            if (pending_st >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (pending_st == 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            // operations younger than the frame's LDS-DMA: the epilogue stores and the window preloads
+            const int younger = pending_st + WP;
+            if (younger >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             stamp(u, 1);
         }
@@ -523,7 +556,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0>(v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw)
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP>(v, a.window_il, a.wide_tw, in_rs,
+                                                                                        tid, planar, lraw, wpre)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
@@ -558,7 +592,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             for (int q = 0; q < PT; q++) asm volatile("" : "+v"(v[q].x), "+v"(v[q].y));
         }
 
-        if (!active) return;
+        if (!active) {
+            load_wpre();
+            return;
+        }
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
         if constexpr (COMPLEX_OUT) {
             const rsrc_t o_rs = make_rsrc(a.complex_out + ((size_t)frame * ss + dit_r) * n, n * 8);
@@ -630,6 +667,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             }
             stamp(u, 6);
         }
+        load_wpre();  // next item's window pairs (the point registers are free now)
     };
     for (int u = u0; u < items; it_count++) {
         int un = dq ? items : next_item(u);  // with the queue, body() dequeues the next item into un
@@ -660,7 +698,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int work = (RS == 1 && CO && a.dit_ss > 1) ? a.n_frames * a.dit_ss : a.n_frames;
+    const int work = (RS == 1 && CO && a.dit_ss > 1) ? ((a.n_frames + 7) / 8) * 8 * a.dit_ss : a.n_frames;
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;

@@ -4,8 +4,9 @@
  * This image has no JDK, so instead of <jni.h> the shim uses this restatement
  * of the JNI specification's primitive types and of the JNINativeInterface
  * function table LAYOUT: the slots the shim calls sit at their specified
- * indices (GetArrayLength 171, GetByteArrayRegion 200, GetFloatArrayRegion 205,
- * SetFloatArrayRegion 213, ExceptionCheck 228); every other slot is opaque.
+ * indices (GetArrayLength 171, GetByteArrayRegion 200, GetIntArrayRegion 203,
+ * GetFloatArrayRegion 205, SetIntArrayRegion 211, SetFloatArrayRegion 213,
+ * ExceptionCheck 228); every other slot is opaque.
  * JNIEnv* points at a pointer to that table, which is binary-identical to both
  * the C and the C++ flavour of <jni.h>.
  */
@@ -32,6 +33,7 @@ typedef void *jobject;
 typedef jobject jarray;
 typedef jarray jfloatArray;
 typedef jarray jbyteArray;
+typedef jarray jintArray;
 
 #define JNI_FALSE 0
 #define JNI_TRUE 1
@@ -44,9 +46,13 @@ struct JNINativeInterface_ {
     jsize(JNICALL *GetArrayLength)(JNIEnv *env, jarray array); /* 171 */
     void *reserved_172_199[28];
     void(JNICALL *GetByteArrayRegion)(JNIEnv *env, jbyteArray array, jsize start, jsize len, jbyte *buf); /* 200 */
-    void *reserved_201_204[4];
+    void *reserved_201_202[2];
+    void(JNICALL *GetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len, jint *buf); /* 203 */
+    void *reserved_204;
     void(JNICALL *GetFloatArrayRegion)(JNIEnv *env, jfloatArray array, jsize start, jsize len, jfloat *buf); /* 205 */
-    void *reserved_206_212[7];
+    void *reserved_206_210[5];
+    void(JNICALL *SetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len, const jint *buf); /* 211 */
+    void *reserved_212;
     void(JNICALL *SetFloatArrayRegion)(JNIEnv *env, jfloatArray array, jsize start, jsize len,
                                        const jfloat *buf); /* 213 */
     void *reserved_214_227[14];
@@ -60,7 +66,9 @@ struct JNINativeInterface_ {
 }
 static_assert(offsetof(JNINativeInterface_, GetArrayLength) == 171 * sizeof(void *), "JNI slot 171");
 static_assert(offsetof(JNINativeInterface_, GetByteArrayRegion) == 200 * sizeof(void *), "JNI slot 200");
+static_assert(offsetof(JNINativeInterface_, GetIntArrayRegion) == 203 * sizeof(void *), "JNI slot 203");
 static_assert(offsetof(JNINativeInterface_, GetFloatArrayRegion) == 205 * sizeof(void *), "JNI slot 205");
+static_assert(offsetof(JNINativeInterface_, SetIntArrayRegion) == 211 * sizeof(void *), "JNI slot 211");
 static_assert(offsetof(JNINativeInterface_, SetFloatArrayRegion) == 213 * sizeof(void *), "JNI slot 213");
 static_assert(offsetof(JNINativeInterface_, ExceptionCheck) == 228 * sizeof(void *), "JNI slot 228");
 static_assert(sizeof(JNINativeInterface_) == RFA_JNI_TABLE_SLOTS * sizeof(void *), "JNI table size");

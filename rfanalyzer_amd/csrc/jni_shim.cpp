@@ -6,6 +6,7 @@
 // (nativedsp.cpp:56-64 -- here a handle, freed instead of leaked), no return
 // value on the legacy void symbols.  The new planar symbol returns JNI_FALSE on
 // a size mismatch like NativeDsp.kt:45-46.
+#include <cstring>
 #include <mutex>
 #include <vector>
 
@@ -108,6 +109,154 @@ JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processIqBytesNati
     if (rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)stride, rows.data()) != RFA_OK) return -1;
     (*env)->SetFloatArrayRegion(env, mag_out, 0, (jsize)rows.size(), rows.data());
     return (jint)n_frames;
+}
+
+// ---------------------------------------------------------------- stateful natives
+static rfa_handle *as_h(jlong h) { return reinterpret_cast<rfa_handle *>(static_cast<intptr_t>(h)); }
+static rfa_ddc *as_d(jlong h) { return reinterpret_cast<rfa_ddc *>(static_cast<intptr_t>(h)); }
+
+JNIEXPORT jlong JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_createAnalyzerNative(
+    JNIEnv *, jobject, jint fft_size, jint input_format, jint window, jint avg_mode, jint avg_length,
+    jfloat ema_alpha, jboolean peak_hold, jint ring_rows, jint device) {
+    rfa_config c;
+    rfa_default_config(&c);
+    c.fft_size = fft_size;
+    c.input_format = input_format;
+    c.window = window;
+    c.avg_mode = avg_mode;
+    c.avg_length = avg_length;
+    c.ema_alpha = ema_alpha;
+    c.peak_hold = peak_hold ? 1 : 0;
+    c.ring_rows = ring_rows;
+    c.device_id = device;
+    rfa_handle *h = nullptr;
+    if (rfa_create(&c, &h) != RFA_OK) return 0;
+    return static_cast<jlong>(reinterpret_cast<intptr_t>(h));
+}
+
+JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_destroyAnalyzerNative(JNIEnv *, jobject, jlong handle) {
+    if (handle) rfa_destroy(as_h(handle));
+}
+
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processPacketNative(
+    JNIEnv *env, jobject, jlong handle, jbyteArray packet, jint frame_stride, jlong frequency, jlong sample_rate) {
+    rfa_handle *h = as_h(handle);
+    if (!h || !packet || frame_stride < 0) return RFA_ERR_INVALID;
+    rfa_config c;
+    if (rfa_get_config(h, &c) != RFA_OK) return RFA_ERR_INVALID;
+    static const int bps_tab[5] = {2, 2, 4, 8, 8};
+    const jsize bytes = (*env)->GetArrayLength(env, packet);
+    const long long frame_bytes = (long long)c.fft_size * bps_tab[c.input_format];
+    const long long stride = frame_stride ? frame_stride : frame_bytes;
+    if (bytes < frame_bytes) return 0;  // a partial frame waits (Scheduler.kt:264-270 fills across packets)
+    const long long n_frames = (bytes - frame_bytes) / stride + 1;
+    int rc = rfa_set_tuning(h, frequency, sample_rate);
+    if (rc != RFA_OK) return rc;
+    std::vector<jbyte> in(bytes);
+    (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
+    rc = rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)stride, nullptr);
+    return rc != RFA_OK ? rc : (jint)n_frames;
+}
+
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_drawPreprocessNative(
+    JNIEnv *env, jobject, jlong handle, jint width, jint fft_height, jlong viewport_frequency,
+    jlong viewport_sample_rate, jfloat min_db, jfloat max_db, jint average_length, jintArray color_map,
+    jintArray color_buffer, jfloatArray fft_path_y, jfloatArray peaks_y, jfloatArray autoscale) {
+    rfa_handle *h = as_h(handle);
+    if (!h || !color_map || !color_buffer || !fft_path_y || !autoscale || width <= 0) return RFA_ERR_INVALID;
+    rfa_config c;
+    if (rfa_get_config(h, &c) != RFA_OK) return RFA_ERR_INVALID;
+    const jsize cm = (*env)->GetArrayLength(env, color_map);
+    if ((*env)->GetArrayLength(env, color_buffer) < (jsize)((long long)c.ring_rows * width) ||
+        (*env)->GetArrayLength(env, fft_path_y) < width || (*env)->GetArrayLength(env, autoscale) < 2 ||
+        (peaks_y && (*env)->GetArrayLength(env, peaks_y) < width) || cm <= 0)
+        return RFA_ERR_SIZE;
+    std::vector<jint> cmap(cm);
+    (*env)->GetIntArrayRegion(env, color_map, 0, cm, cmap.data());
+    rfa_draw_params p;
+    std::memset(&p, 0, sizeof(p));
+    p.width = width;
+    p.fft_height = fft_height;
+    p.viewport_frequency = viewport_frequency;
+    p.viewport_sample_rate = viewport_sample_rate;
+    p.min_db = min_db;
+    p.max_db = max_db;
+    p.average_length = average_length;
+    p.colormap = reinterpret_cast<const uint32_t *>(cmap.data());
+    p.colormap_size = cm;
+    std::vector<uint32_t> colors((size_t)c.ring_rows * width);
+    std::vector<float> path(width), pk(peaks_y ? width : 0);
+    float mm[2] = {0, 0};
+    const int rc = rfa_draw_preprocess(h, &p, colors.data(), path.data(), peaks_y ? pk.data() : nullptr, mm);
+    if (rc != RFA_OK) return rc;
+    (*env)->SetIntArrayRegion(env, color_buffer, 0, (jsize)colors.size(), reinterpret_cast<const jint *>(colors.data()));
+    (*env)->SetFloatArrayRegion(env, fft_path_y, 0, width, path.data());
+    if (peaks_y) (*env)->SetFloatArrayRegion(env, peaks_y, 0, width, pk.data());
+    (*env)->SetFloatArrayRegion(env, autoscale, 0, 2, mm);
+    return RFA_OK;
+}
+
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_rowWindowStatsNative(JNIEnv *env, jobject, jlong handle,
+                                                                                  jintArray lo, jintArray hi,
+                                                                                  jfloatArray peak, jfloatArray avg) {
+    rfa_handle *h = as_h(handle);
+    if (!h || !lo || !hi || !peak || !avg) return RFA_ERR_INVALID;
+    const jsize n = (*env)->GetArrayLength(env, lo);
+    if ((*env)->GetArrayLength(env, hi) != n || (*env)->GetArrayLength(env, peak) < n ||
+        (*env)->GetArrayLength(env, avg) < n)
+        return RFA_ERR_SIZE;
+    std::vector<jint> l(n), u(n);
+    std::vector<float> pk(n), av(n);
+    (*env)->GetIntArrayRegion(env, lo, 0, n, l.data());
+    (*env)->GetIntArrayRegion(env, hi, 0, n, u.data());
+    const int rc = rfa_row_window_stats(h, l.data(), u.data(), (size_t)n, pk.data(), av.data());
+    if (rc != RFA_OK) return rc;
+    (*env)->SetFloatArrayRegion(env, peak, 0, n, pk.data());
+    (*env)->SetFloatArrayRegion(env, avg, 0, n, av.data());
+    return RFA_OK;
+}
+
+JNIEXPORT jlong JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcCreate(JNIEnv *, jobject, jint input_format,
+                                                                         jint sample_rate, jint output_rate,
+                                                                         jboolean resampler, jint device) {
+    rfa_ddc *d = nullptr;
+    const int rc = resampler ? rfa_ddc_create_resampler(device, input_format, sample_rate, output_rate, &d)
+                             : rfa_ddc_create(device, input_format, sample_rate, output_rate, &d);
+    return rc == RFA_OK ? static_cast<jlong>(reinterpret_cast<intptr_t>(d)) : 0;
+}
+
+JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcDestroy(JNIEnv *, jobject, jlong handle) {
+    if (handle) rfa_ddc_destroy(as_d(handle));
+}
+
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcSetFrequencies(JNIEnv *, jobject, jlong handle,
+                                                                                jlong frequency,
+                                                                                jlong channel_frequency) {
+    rfa_ddc *d = as_d(handle);
+    return d ? rfa_ddc_set_frequencies(d, frequency, channel_frequency) : RFA_ERR_INVALID;
+}
+
+JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_ddcProcess(JNIEnv *env, jobject, jlong handle,
+                                                                         jbyteArray packet, jfloatArray re,
+                                                                         jfloatArray im) {
+    rfa_ddc *d = as_d(handle);
+    if (!d || !packet || !re || !im) return RFA_ERR_INVALID;
+    const jsize bytes = (*env)->GetArrayLength(env, packet);
+    const jsize cap = (*env)->GetArrayLength(env, re);
+    if ((*env)->GetArrayLength(env, im) < cap) return RFA_ERR_SIZE;
+    static const int bps_tab[4] = {2, 2, 4, 8};
+    int32_t fmt = 0;  // the handle's input format gives the packet's bytes per sample
+    if (rfa_ddc_get_format(d, &fmt) != RFA_OK || fmt < 0 || fmt > 3) return RFA_ERR_INVALID;
+    const size_t n_samples = (size_t)bytes / bps_tab[fmt];
+    std::vector<jbyte> in(bytes);
+    (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
+    std::vector<float> r((size_t)cap), q((size_t)cap);
+    size_t got = 0;
+    const int rc = rfa_ddc_process_host(d, in.data(), n_samples, r.data(), q.data(), (size_t)cap, &got);
+    if (rc != RFA_OK) return rc;
+    (*env)->SetFloatArrayRegion(env, re, 0, (jsize)got, r.data());
+    (*env)->SetFloatArrayRegion(env, im, 0, (jsize)got, q.data());
+    return (jint)got;
 }
 
 }  // extern "C"

@@ -22,3 +22,24 @@ def rfa():
     n = rfanalyzer_amd.device_count()
     assert n > 0, "no HIP device visible to librfa"
     return rfanalyzer_amd
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Make the parity bar visible: every dB comparison of the session, the share of
+    bins the Parseval floor excluded, and the worst difference over all finite bins."""
+    try:
+        import golden_util as gu
+    except ImportError:
+        return
+    log = gu.PARITY_LOG
+    if not log:
+        return
+    tr = terminalreporter
+    tr.write_sep("-", "dB parity (tests/golden_util.py db_stats)")
+    for floor in sorted({x["floor_db"] for x in log}):
+        xs = [x for x in log if x["floor_db"] == floor]
+        tr.write_line(f"floor {floor:.0f} dB: {len(xs)} comparisons, {sum(x['bins'] for x in xs)} bins; "
+                      f"max |d| live {max(x['max_live'] for x in xs):.2e} dB (bar {gu.DB_TOL}); "
+                      f"excluded below floor: mean {sum(x['excluded'] for x in xs) / len(xs):.3f}, "
+                      f"max {max(x['excluded'] for x in xs):.3f}; "
+                      f"max |d| over all finite bins {max(x['max_finite'] for x in xs):.3e} dB")

@@ -78,9 +78,20 @@ def pffft_diff(got: np.ndarray, exp: np.ndarray) -> float:
     return db_diff(got, exp, FLOOR_PFFFT_DB)
 
 
-def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> float:
-    """Max |dB difference| over bins within floor_db (default FLOOR_DB) of the row's total level.
+# Every db_diff call appends its statistics here; tests/conftest.py prints a
+# summary at the end of the session (how many bins the floor excluded, and the
+# worst difference over ALL finite bins, not only the live ones).
+PARITY_LOG: list[dict] = []
 
+
+def db_stats(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> dict:
+    """The parity numbers of one comparison:
+
+    ``max_live``    max |dB difference| over bins within floor_db (default FLOOR_DB) of
+                    the row's total (Parseval) level -- the 0.01 dB bar;
+    ``excluded``    fraction of finite bins below that floor (not held to the bar);
+    ``max_finite``  max |dB difference| over every bin finite on both sides;
+    ``bins``        bins compared.
     Raises AssertionError on a structural mismatch: -inf vs finite above the
     floor, a NaN, or a deep bin on one side that is shallow on the other."""
     got = np.atleast_2d(np.asarray(got, np.float32))
@@ -88,7 +99,8 @@ def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> 
     assert got.shape == exp.shape, (got.shape, exp.shape)
     assert not np.isnan(got).any(), "NaN in output"
     floor = FLOOR_DB if floor_db is None else floor_db
-    worst = 0.0
+    worst = worst_all = 0.0
+    excluded = finite_bins = 0
     for g, e in zip(got, exp):
         if np.all(np.isneginf(e)):
             assert np.all(np.isneginf(g)), "expected an all -inf row (all-zero input)"
@@ -98,7 +110,31 @@ def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> 
         live = e >= top - floor
         assert np.all(np.isfinite(g[live])), "non-finite bin above the floor"
         worst = max(worst, float(np.max(np.abs(g[live] - e[live]))))
+        fin = np.isfinite(g) & np.isfinite(e)
+        finite_bins += int(fin.sum())
+        excluded += int((fin & ~live).sum())
+        if fin.any():
+            worst_all = max(worst_all, float(np.max(np.abs(g[fin] - e[fin]))))
         deep = ~live
         if deep.any():
             assert np.all(g[deep] < top - floor + 20.0), "deep bin came out shallow"
-    return worst
+    st = {"floor_db": floor, "max_live": worst, "max_finite": worst_all, "bins": int(got.size),
+          "excluded": excluded / finite_bins if finite_bins else 0.0}
+    PARITY_LOG.append(st)
+    return st
+
+
+def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> float:
+    """Max |dB difference| over bins within floor_db (default FLOOR_DB) of the row's
+    total level (db_stats' ``max_live``); the call is recorded in PARITY_LOG."""
+    return db_stats(got, exp, floor_db)["max_live"]
+
+
+def full_row_diff(got: np.ndarray, exp: np.ndarray) -> float:
+    """Max |dB difference| over EVERY bin (no floor); -inf must match -inf."""
+    got = np.atleast_2d(np.asarray(got, np.float32))
+    exp = np.atleast_2d(np.asarray(exp, np.float32))
+    assert got.shape == exp.shape
+    assert np.array_equal(np.isneginf(got), np.isneginf(exp)), "-inf bins differ"
+    fin = np.isfinite(exp)
+    return float(np.max(np.abs(got[fin] - exp[fin])))

@@ -1,7 +1,8 @@
 """A mock JNIEnv built with ctypes: a 233-slot JNINativeInterface table whose
-GetArrayLength (171), GetByteArrayRegion (200), GetFloatArrayRegion (205),
-SetFloatArrayRegion (213) and ExceptionCheck (228) slots are Python callbacks
-over numpy arrays.  Java arrays are represented by integer handles."""
+GetArrayLength (171), GetByteArrayRegion (200), GetIntArrayRegion (203),
+GetFloatArrayRegion (205), SetIntArrayRegion (211), SetFloatArrayRegion (213)
+and ExceptionCheck (228) slots are Python callbacks over numpy arrays.  Java
+arrays are represented by integer handles (0 = null)."""
 import ctypes
 
 import numpy as np
@@ -22,11 +23,13 @@ class MockJNIEnv:
             _GETLEN(self._get_len),
             _GETREG(self._get_region),
             _GETREG(self._get_region),
+            _GETREG(self._get_region),
+            _GETREG(self._set_region),
             _GETREG(self._set_region),
             _EXC(lambda env: 0),
         ]
         table = (ctypes.c_void_p * SLOTS)()
-        for slot, cb in zip((171, 200, 205, 213, 228), self._cbs):
+        for slot, cb in zip((171, 200, 203, 205, 211, 213, 228), self._cbs):
             table[slot] = ctypes.cast(cb, ctypes.c_void_p)
         self.table = table
         self.table_ptr = ctypes.c_void_p(ctypes.addressof(table))
@@ -48,6 +51,6 @@ class MockJNIEnv:
         ctypes.memmove(buf, a[start:start + length].ctypes.data, length * a.itemsize)
 
     def _set_region(self, env, arr, start, length, buf):
-        self.calls.append("SetFloatArrayRegion")
+        self.calls.append("SetFloatArrayRegion" if self.arrays[arr].dtype == np.float32 else "SetIntArrayRegion")
         a = self.arrays[arr]
         ctypes.memmove(a[start:start + length].ctypes.data, buf, length * a.itemsize)

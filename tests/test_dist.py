@@ -34,10 +34,12 @@ def _worker(rank, world, port, q):
     import torch
     import torch.distributed as dist
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import bench
+
+    ranks = bench.Ranks(dry=True)  # bench.py's process group (gloo here, RCCL on GPUs)
     try:
-        import bench
 
         data = _data()
         s, e = sharding.frame_range(FRAMES, rank, world)
@@ -46,13 +48,13 @@ def _worker(rank, world, port, q):
         mine = torch.from_numpy(np.stack([rows.max(0), decay, b, fresh]).astype(np.float32))
         parts = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine)  # host-side state hand-off (test only; the bench has none)
-        slowest = bench.max_over_ranks(float(rank + 1), world, torch.device("cpu"))
+        slowest = max(ranks.all_values(float(rank + 1)))  # bench.py's max-over-ranks timing
         if rank == 0:
             pk = sharding.peak_combine([p[0].numpy() for p in parts])
             em = sharding.ema_combine(None, [(p[1].numpy(), p[2].numpy(), p[3].numpy()) for p in parts])
             q.put((pk, em, slowest))
     finally:
-        dist.destroy_process_group()
+        ranks.close()
 
 
 @pytest.mark.parametrize("world", [2])

@@ -112,3 +112,15 @@ def test_file_framing_config1():
     assert 4_000_000 - 15 * 262_144 == 67_840
     big = processor.file_frames(4_000_000, 262_144, 2, 262_144)  # N > packet samples: 2 packets/frame
     assert len(big) == 7 and big[1][0] == 2 * 262_144
+
+
+def test_config1_fixture_full_row_bar():
+    """Config 1 replay fixture: the float64 restatement is within 0.01 dB of the
+    reference's pffft rows on EVERY bin (no Parseval floor), so the GPU test can hold
+    the product to the full-row bar too (tests/test_gpu_parity.py)."""
+    spec = next(s for s in MANIFEST["fixtures"] if s["name"] == "file_s8_2msps_n1024")
+    data = gu.fixture_input(spec)
+    ref64 = oracle.spectrum_rows(data, oracle.IN_S8, 1024, 15, spec["packet_size"], oracle.WIN_BLACKMAN)
+    st = gu.db_stats(ref64, gu.expected(spec), gu.FLOOR_PFFFT_DB)
+    assert st["excluded"] < 0.001  # 2 of 15 360 bins fall below the 45 dB floor
+    assert gu.full_row_diff(ref64, gu.expected(spec)) <= gu.DB_TOL
