@@ -674,32 +674,23 @@ hipError_t launch_boxcar(const float *ring, int rows, int n, int logrs, int read
     return hipGetLastError();
 }
 
-// Streaming copy at the HBM ceiling (bench denominator): 4 float4 per lane in
-// flight, grid-stride over 16-KiB blocks per workgroup iteration.
+// Streaming copy at the HBM ceiling (bench denominator): one float4 per lane, one
+// pass over the buffer (the fastest of the shapes in
+// profiles/r02a/copy_kernel_variants.txt: 6.2 TB/s read + write on MI355X).
 __global__ void __launch_bounds__(256) stream_copy_kernel(float4 *__restrict__ dst, const float4 *__restrict__ src,
                                                           long long n4) {
-    constexpr int U = 4;
-    const long long stride = (long long)gridDim.x * 256 * U;
-    for (long long base = (long long)blockIdx.x * 256 * U + threadIdx.x; base < n4; base += stride) {
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (base + u * 256 < n4) v[u] = src[base + u * 256];
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (base + u * 256 < n4) dst[base + u * 256] = v[u];
-    }
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i < n4) dst[i] = src[i];
 }
 
 hipError_t launch_stream_copy(void *dst, const void *src, size_t bytes, hipStream_t s) {
     const long long n4 = (long long)(bytes / 16);
     if (n4 <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const long long blocks = std::min<long long>((n4 + 1023) / 1024, (long long)cus * 8);
-    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<float4 *>(dst),
-                       static_cast<const float4 *>(src), n4);
+    for (long long off = 0; off < n4; off += (long long)0x7fffffff / 256 * 256) {  // grid.x limit
+        const long long cnt = std::min<long long>(n4 - off, (long long)0x7fffffff / 256 * 256);
+        hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, s,
+                           static_cast<float4 *>(dst) + off, static_cast<const float4 *>(src) + off, cnt);
+    }
     return hipGetLastError();
 }
 

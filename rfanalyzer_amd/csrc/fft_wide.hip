@@ -212,7 +212,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // arrive preloaded in wpre[idx] (issued by the previous item's tail, see
 // fft_wide_kernel); the rest are loaded here, behind the preloaded chunks' work.
 #ifndef RFA_WPRE
-#define RFA_WPRE 0  // measured slower at 8/16/32 (profiles/r02/window_preload_ab.txt): spills
+#define RFA_WPRE 0  // measured slower at 8/16/32 (profiles/r02a/window_preload_and_stagger_ab.txt): spills
 #endif
 template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,

@@ -4,12 +4,18 @@
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md
 (HBM section) FETCH_SIZE counts 64 B per 128-B read request on gfx950, so it is
 doubled; WRITE_SIZE is taken as reported.  Both count Infinity-Cache hits too.
-usage: pmc_summary.py FETCH_CSV WRITE_CSV KEY KERNEL_SUBSTR [OUT_JSON]
+usage: pmc_summary.py FETCH_CSV WRITE_CSV KEY KERNEL_SUBSTR [OUT_JSON [SOURCE_LABEL]]
+The record carries the sha256 (16 hex) of the librfa.so measured (RFA_LIB or the
+in-tree build): bench.py reports it as roofline.traffic only for that exact build.
 """
 import csv
+import hashlib
 import json
+import os
 import statistics
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_dispatch(path, counter, kernel):
@@ -24,6 +30,10 @@ def per_dispatch(path, counter, kernel):
 def main():
     fetch_csv, write_csv, key, kernel = sys.argv[1:5]
     out = sys.argv[5] if len(sys.argv) > 5 else None
+    source = sys.argv[6] if len(sys.argv) > 6 else os.path.dirname(fetch_csv)
+    lib = os.environ.get("RFA_LIB") or os.path.join(ROOT, "rfanalyzer_amd", "librfa.so")
+    with open(lib, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()[:16]
     f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
     w = per_dispatch(write_csv, "WRITE_SIZE", kernel)
     if not f or not w:
@@ -32,7 +42,7 @@ def main():
     write = statistics.median(w) * 1024
     rec = {"kernel": kernel, "dispatches": [len(f), len(w)],
            "fetch_bytes_per_launch": round(fetch), "write_bytes_per_launch": round(write),
-           "hbm_bytes_per_launch": round(fetch + write),
+           "hbm_bytes_per_launch": round(fetch + write), "librfa_sha16": sha, "source": source,
            "note": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B), WRITE_SIZE as reported; "
                    "both include Infinity-Cache hits"}
     print(json.dumps({key: rec}, indent=1))
