@@ -72,6 +72,8 @@ def parse(argv=None):
     p.add_argument("--f32-steps", type=int, default=4, help="steps of the float32-input companion run (0 = skip)")
     p.add_argument("--demod-steps", type=int, default=5,
                    help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
+    p.add_argument("--profile-every", type=int, default=8,
+                   help="HIP-event timing of every K-th main-kernel launch in the timed region (1 = all)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--dry-run", action="store_true", help="no GPU: launcher / barrier / timing path only (gloo)")
     a = p.parse_args(argv)
@@ -214,18 +216,25 @@ def run_streams(args, ranks, fmt, steps, warmup, seed):
 
     ptrs = [b.data_ptr() for b in pool]
 
+    every, sampling = max(1, args.profile_every), [False]
+
     def step(_k):
         for _ in range(calls):  # rfa_process on the torch stream set above (no per-call Python stream lookup)
-            eng.process_device(ptrs[ctr[0] % len(ptrs)], frames, 0, None)
+            if sampling[0] and ctr[0] % every == 0:  # events around a sample of the launches
+                eng.set_profiling(True)
+                eng.process_device(ptrs[ctr[0] % len(ptrs)], frames, 0, None)
+                eng.set_profiling(False)
+            else:
+                eng.process_device(ptrs[ctr[0] % len(ptrs)], frames, 0, None)
             ctr[0] += 1
 
     for _ in range(warmup):  # untimed, before the kernel clock starts
         step(0)
-    eng.set_profiling(True)
     ms0, l0 = eng.kernel_time()
+    sampling[0] = True
     slow, per = timed(ranks, step, steps, 0)
+    sampling[0] = False
     ms1, l1 = eng.kernel_time()
-    eng.set_profiling(False)
     name = eng.main_kernel_name()
     eng.close()
     del pool
@@ -259,10 +268,17 @@ def run_shard(args, ranks, steps, warmup):
 
     ptrs, rows_ptr = [b.data_ptr() for b in pool], rows.data_ptr()
 
+    every, sampling = max(1, args.profile_every), [False]
+
     def step(_k):
         for _ in range(calls):
             if mine:
+                prof = sampling[0] and ctr[0] % every == 0
+                if prof:
+                    eng.set_profiling(True)
                 eng.process_device(ptrs[ctr[0] % len(ptrs)], mine, 0, rows_ptr)
+                if prof:
+                    eng.set_profiling(False)
             if gathered is not None:
                 padded[:mine * n].copy_(rows[:mine * n])
                 ranks.dist.all_gather(gathered, padded)
@@ -270,11 +286,11 @@ def run_shard(args, ranks, steps, warmup):
 
     for _ in range(warmup):
         step(0)
-    eng.set_profiling(True)
     ms0, l0 = eng.kernel_time()
+    sampling[0] = True
     slow, per = timed(ranks, step, steps, 0)
+    sampling[0] = False
     ms1, l1 = eng.kernel_time()
-    eng.set_profiling(False)
     name = eng.main_kernel_name()
     eng.close()
     return slow, per, (ms1 - ms0) / max(1, l1 - l0), name, (s, e)
@@ -558,7 +574,8 @@ def main():
                           "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                           "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
                           "alg_bytes_per_launch": alg_bytes,
-                          "timing": "HIP events on the handle stream around every main-kernel launch of the timed region"}
+                          "timing": f"HIP events on the handle stream around every {max(1, args.profile_every)}-th "
+                                    "main-kernel launch of the timed region"}
     single = ranks.rank == 0 and ranks.world == 1 and not args.dry_run
     if single:
         tr, src = pmc_traffic(args, fmt, n, frames)

@@ -242,8 +242,9 @@ RFA_API int rfa_fft_logmag_interleaved(rfa_handle *h, const float *in, float *ma
 /* nativedsp.cpp:19-42: ordered, unscaled, forward complex FFT, 2N floats each. */
 RFA_API int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n);
 
-/* Profiling: when enabled, HIP events bracket every main FFT kernel launch on
- * the handle stream and the summed device time is reported. */
+/* Profiling: while enabled, HIP events bracket every main FFT kernel launch on
+ * the handle stream; rfa_get_kernel_time waits for and sums them.  Toggling
+ * never synchronises, so a caller may profile a sample of its launches. */
 /* Measurement support (no reference counterpart).  rfa_stream_copy: the device
  * stream-copy kernel whose rate is the measured bandwidth ceiling SURVEY.md
  * §8(d) asks the bench to report beside the 8 TB/s spec (float4 loads and

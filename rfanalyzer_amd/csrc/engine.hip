@@ -52,6 +52,8 @@ struct rfa_handle {
     int max_logm = 14;                // RFA_MAX_LOGM experiment switch
     int wide_big = 15;                // RFA_WIDE_LOGM: 15 (32 K workgroups) or 14 for N > 16 K
     int ring_logrs = 0;               // ring row order (fft_kernels.h ring_pos): residue split of the main kernel
+    int w64 = 0;                      // RFA_W64=1: the four-step wave kernel at N = 64 K (opt-in)
+    int prio = 0;                     // RFA_W64_PRIO (speed only)
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
@@ -265,6 +267,8 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         a.stamps = h->d_stamps;
     }
     a.wide_big = h->wide_big;
+    a.w64 = h->w64;
+    a.prio = h->prio;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
     if (a.window == h->d_window) a.window_il = h->d_window_il;
@@ -473,9 +477,14 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
     // ring row order: residue-major when the wide kernel splits N into residue
     // sub-FFTs (whole-line stores per workgroup); RFA_RING_NATURAL=1 keeps natural order
+    if (const char *d = std::getenv("RFA_W64")) h->w64 = std::atoi(d) != 0;
+    if (const char *d = std::getenv("RFA_W64_PRIO")) h->prio = std::atoi(d);
     if (h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(logn) && logn <= 17) {
         const char *nat = std::getenv("RFA_RING_NATURAL");
-        if (!(nat && std::atoi(nat) != 0)) h->ring_logrs = logn - rfa::wide_logm(logn, h->wide_big);
+        if (nat && std::atoi(nat) != 0) h->w64 = 0;  // the wave kernel only writes its own order
+        else h->ring_logrs = rfa::ring_logrs_for(logn, h->wide_big, h->w64);
+    } else {
+        h->w64 = 0;
     }
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
@@ -1093,7 +1102,9 @@ int rfa_stream_copy(void *dst, const void *src, size_t bytes, void *stream) {
 
 int rfa_set_profiling(rfa_handle *h, int enable) {
     if (!h) return RFA_ERR_INVALID;
-    if (!enable && h->profile) drain_events(h, true);
+    // no drain here (that would synchronise): pending pairs are collected by the
+    // next profiled launch or by rfa_get_kernel_time, so profiling can be toggled
+    // around single launches (sampled timing) without stalling the stream
     h->profile = enable != 0;
     return RFA_OK;
 }

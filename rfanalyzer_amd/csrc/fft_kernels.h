@@ -19,6 +19,10 @@ namespace rfa {
 __host__ __device__ __forceinline__ int ring_pos(int t, int logrs, int logm) {
     return ((t & ((1 << logrs) - 1)) << logm) | (t >> logrs);
 }
+// inverse: the natural (fft-shifted) bin stored at ring element p
+__host__ __device__ __forceinline__ int ring_bin(int p, int logrs, int logm) {
+    return ((p & ((1 << logm) - 1)) << logrs) | (p >> logm);
+}
 
 // Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
 // 128 KiB + padding, one workgroup per CU).  Larger N split across
@@ -58,6 +62,8 @@ struct FftLaunch {
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
     int stage = 1;            // wide kernel: LDS-DMA staged 8/16-bit input when aligned (RFA_STAGE=0 disables)
+    int w64 = 0;              // N = 64 K: the four-step "wave" kernel (RFA_W64=1, opt-in; ring_logrs 6)
+    int prio = 0;             // w64 kernel: s_setprio 1 for waves with (wave & prio) != 0 (RFA_W64_PRIO, speed only)
     // staged one-residue kernels: work-queue counter [0] + finisher count [1], zero at
     // launch and zeroed again by the kernel's last workgroup (null = static item stride)
     unsigned *queue = nullptr;
@@ -72,6 +78,8 @@ struct FftLaunch {
 hipError_t launch_fft(const FftLaunch &a);
 // The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
 bool wide_supported(int logn);
+// ring order (ring_pos logrs) the main kernel writes for N = 2^logn
+int ring_logrs_for(int logn, int wide_big, int w64);
 constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
 // sub-FFT size of the wide kernel: N itself up to 16 K, else 2^big (15: one
 // 32 K-point workgroup per CU; 14: 16 K, two per CU) with N / 2^big residues

@@ -400,30 +400,21 @@ __device__ __forceinline__ const float *state_row(const StateLaunch &a, int f) {
 __device__ __forceinline__ int state_logrs(const StateLaunch &a) { return a.ring_rows > 0 ? a.ring_logrs : 0; }
 __device__ __forceinline__ int ilog2_dev(int n) { return 31 - __clz(n); }
 
-// Fft-shifted bins [t, t+4) of a row (t a multiple of 4): one 16-B load in natural
-// order; in the residue-major ring (ring_pos) two 8-B loads for RS = 2 (bins t, t+2
-// in residue 0's block, t+1, t+3 in residue 1's) or a gather for RS = 4.
-__device__ __forceinline__ float4 load_bins4(const float *row, int t, int logrs, int logm) {
-    if (logrs == 0) return *reinterpret_cast<const float4 *>(row + t);
-    if (logrs == 1) {
-        const float2 a0 = *reinterpret_cast<const float2 *>(row + (t >> 1));
-        const float2 a1 = *reinterpret_cast<const float2 *>(row + (1 << logm) + (t >> 1));
-        return make_float4(a0.x, a1.x, a0.y, a1.y);
-    }
-    return make_float4(row[ring_pos(t, logrs, logm)], row[ring_pos(t + 1, logrs, logm)],
-                       row[ring_pos(t + 2, logrs, logm)], row[ring_pos(t + 3, logrs, logm)]);
-}
+// The state kernels walk the rows in STORAGE order (ring_pos order when they read
+// the ring, natural order for caller / staging rows): every row load is a
+// contiguous 16-B load, and the element at storage position p updates the peak /
+// EMA of natural bin ring_bin(p) (peaks and EMA are kept in natural order).
 
 // Sequential peak-hold / EMA over the batch (one thread per bin, frames in order).
 // Peak: FftProcessor.kt:229-232.  EMA (extension): em += alpha (x - em); an
 // uninitialised (-inf) average takes the frame's value.
 __global__ void state_kernel(StateLaunch a) {
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
-    if (bin >= a.n) return;
+    const int pos = blockIdx.x * blockDim.x + threadIdx.x;  // storage position
+    if (pos >= a.n) return;
+    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ilog2_dev(a.n) - lr);
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     const float al = a.ema_alpha;
-    const int lr = state_logrs(a), pos = ring_pos(bin, lr, ilog2_dev(a.n) - lr);
 #pragma unroll 8
     for (int f = 0; f < a.n_frames; f++) {
         const float x = state_row(a, f)[pos];
@@ -448,7 +439,6 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
     if (bin >= a.n) return;
     const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
     const float al = a.ema_alpha, keep = 1.0f - al;
-    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float pk[4], emi[4], b[4];
     bool restart[4];
 #pragma unroll
@@ -456,7 +446,7 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
     float am = 1.0f;
 #pragma unroll 4
     for (int f = f0; f < f1; f++) {
-        const float4 x4 = load_bins4(state_row(a, f), bin, lr, lm);
+        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -474,12 +464,13 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
 }
 
 __global__ void state_combine_kernel(StateLaunch a, int chunks) {
-    const int bin = blockIdx.x * blockDim.x + threadIdx.x;
-    if (bin >= a.n) return;
+    const int pos = blockIdx.x * blockDim.x + threadIdx.x;  // storage position of the partials
+    if (pos >= a.n) return;
+    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ilog2_dev(a.n) - lr);
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     for (int c = 0; c < chunks; c++) {
-        const float4 p = a.part[(size_t)c * a.n + bin];
+        const float4 p = a.part[(size_t)c * a.n + pos];
         pk = fmaxf(pk, p.x);
         em = (em == -INFINITY || p.y < 0.0f) ? p.w : fmaf(p.y, em, p.z);
     }
@@ -499,7 +490,6 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     const int bin = blockIdx.x * BPB + 4 * l;
     const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
     const float al = a.ema_alpha, keep = 1.0f - al;
-    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float pk[4], emi[4], b[4];
     bool restart[4];
 #pragma unroll
@@ -507,7 +497,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     float am = 1.0f;
 #pragma unroll 4
     for (int f = f0; f < f1; f++) {
-        const float4 x4 = load_bins4(state_row(a, f), bin, lr, lm);
+        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -522,8 +512,9 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
 #pragma unroll
     for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
     __syncthreads();
+    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     for (int i = threadIdx.x; i < BPB; i += 256) {
-        const int gb = blockIdx.x * BPB + i;
+        const int gb = ring_bin(blockIdx.x * BPB + i, lr, lm);  // natural bin of storage position
         float p = a.peaks ? a.peaks[gb] : 0.f;
         float em = a.ema ? a.ema[gb] : 0.f;
 #pragma unroll

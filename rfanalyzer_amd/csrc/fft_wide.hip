@@ -214,7 +214,10 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_WPRE
 #define RFA_WPRE 0  // measured slower at 8/16/32 (profiles/r02a/window_preload_and_stagger_ab.txt): spills
 #endif
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0>
+// PADRAW (fft_w64_kernel): the staged frame sits in LDS as 8 KiB pieces at a
+// 8448-B pitch (one piece per wave region), i.e. raw element e at e + (e >> 12) * 128.
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0,
+          bool PADRAW = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
                                          const float2 *wpre = nullptr) {
@@ -252,7 +255,10 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
 #pragma unroll
             for (int j = 0; j < RS; j++) {
-                if constexpr (STG) raw[s][q][j] = lraw_t[mo + j * M];  // frame staged in LDS
+                if constexpr (STG) {  // frame staged in LDS
+                    const int e = mo + j * M;
+                    raw[s][q][j] = lraw_t[PADRAW ? e + (e >> 12) * 128 : e];
+                }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
             if constexpr (NOWIN) {  // ablation (RFA_DIAG=16): constant window, no window loads
@@ -720,6 +726,281 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// N = 64 K "wave" kernel.  The 32 K-point sub-FFT of residue r
+// (same decimation-in-frequency pre-stage as fft_wide_kernel) runs as a four-step
+// 32 x 1024 transform whose 1024-point halves belong to half-waves, so only ONE
+// exchange needs the whole workgroup:
+//   m = m1 + 1024 m2, k = k2 + 32 k1
+//   step 1, thread m1 = tid:  z[k2] = DFT32_m2(y[m1 + 1024 m2]) * W_M^(m1 k2)
+//   exchange 0 (workgroup, two half-rounds): half-wave k2 = tid >> 5 gathers z_m1[k2]
+//   step 2, half-wave k2, lane a = tid & 31, m1 = a + 32 b, k1 = c + 32 d:
+//     pass A: DFT32 over b, * W_1024^(a c); transpose inside the wave through its own
+//     8 KiB of LDS (no s_barrier); pass B: DFT32 over a -> Y[k2 + 32 c + 1024 d] in lane c
+// After its transpose a wave's LDS region is free and the wave stages its 8 KiB
+// piece of the next frame there (LDS-DMA), then writes its outputs: residue r's
+// bins k2 + 32 (c + 32 d) are ring block r + 2 k2 (ring_pos order, logrs 6), so
+// every store instruction covers whole 128-B lines.  Caller rows (natural order)
+// take scattered stores; that path is not the hot one.
+// STATUS: opt-in (RFA_W64=1), measured SLOWER than fft_wide_kernel's residue path
+// (134 vs 95 us per 500 frames, profiles/r02a/w64_wave_kernel_ab.txt): hipcc spills
+// 29-40 dwords per thread here (ScratchSize 116 / 160 B), and every scratch reload
+// behind the epilogue's stores waits for them (vmcnt counts in issue order).  Kept,
+// tested (tests/test_gpu_state.py), for the next attempt at the register budget.
+#ifndef RFA_W64_ABL
+#define RFA_W64_ABL 0  // compile-time ablations (register-pressure study only): 1 no step-1 twiddle,
+                       // 2 no exchange 0, 4 no transpose, 8 no pass-A twiddle, 16 ring-only epilogue
+#endif
+template <int FMT, bool STG>
+__global__ void __launch_bounds__(1024, 4) fft_w64_kernel(FftLaunch a) {
+    constexpr int LOGM = 15, PT = 32, RS = 2;
+    using G = WGeo<LOGM, PT>;
+    constexpr int M = G::M;    // 32768
+    constexpr int n = M * RS;  // 65536
+    constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
+    static_assert(G::TPF == 1024 && G::R1 == 32 && G::R2 == 32, "32 x 32 x 32 plan");
+    static_assert(!STG || n * BPS == 16 * 8192, "staged: one 8 KiB piece of the frame per wave");
+    // per-wave LDS region: 1056 points (8 KiB + 256 B): the wave's staged piece, then
+    // its transposes (two 16 x 33 blocks); 16 regions fill the exchange buffer
+    constexpr int WREG = 1056;
+    static_assert(16 * WREG <= G::HALFP && 16 * 1024 <= G::HALFP, "exchange buffer");
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *twp1 = lds;
+    float2 *twp2 = lds + G::TW_P1;
+    float2 *buf = lds + G::TW_LDS;  // 16 K points: staged frame / exchange 0 / per-wave transposes
+    for (int e = threadIdx.x; e < G::TW_LDS; e += 1024) lds[e] = a.wide_tw[e];
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int items = ((a.n_frames + 7) / 8) * 8 * RS;
+    __syncthreads();  // twiddle tables in LDS
+    if (a.prio && (wave & a.prio)) __builtin_amdgcn_s_setprio(1);
+    // blocks b, b+8, ... share an XCD: a frame's two residues run there (speed only)
+    auto frame_of = [&](int u) { return (u / (8 * RS)) * 8 + (u & 7); };
+    // this wave's 8 KiB piece of a frame's raw bytes into its own region of buf
+    // (1 KiB LDS-DMA per instruction; inline asm for the reason given at stage_frame)
+    auto stage_piece = [&](int f) {
+        if constexpr (STG) {
+            const rsrc_t rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * BPS);
+            const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)(uint8_t *)buf;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int c = wave * 8 + j;  // 1 KiB piece c of the frame -> this wave's region
+                unsigned keep;
+                asm volatile(
+                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                    "buffer_load_dwordx4 %2, %3, %4 offen " STG_POLICY "lds\n\ts_mov_b32 m0, %0"
+                    : "=&s"(keep)
+                    : "s"(base + wave * (WREG * 8) + j * 1024), "v"((tid & 63) * 16), "s"(rs), "s"(c * 1024)
+                    : "memory");
+            }
+        }
+    };
+    const int u0 = blockIdx.x;
+    if (u0 < items && frame_of(u0) < a.n_frames) stage_piece(frame_of(u0));
+    int pending = 0;  // this wave's vector-memory operations issued after its last DMA piece
+    for (int u = u0; u < items; u += gridDim.x) {
+        int z;  // opaque zero: keeps the LDS twiddle reads inside the item loop (VGPR budget)
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
+        // opaque thread index: every lane-dependent address is rebuilt per item instead of
+        // being hoisted out of the loop into VGPRs that stay live across the whole item
+        int tq;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(tq) : "v"(tid));
+        const int k2 = tq >> 5;   // step-2 sub-FFT of this half-wave
+        const int l32 = tq & 31;  // lane in the half-wave
+        const int g = u / (8 * RS), rem = u - g * (8 * RS);
+        const int r = rem >> 3, frame = g * 8 + (rem & 7);
+        const bool active = frame < a.n_frames;
+        const rsrc_t in_rs =
+            make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride, active ? (unsigned)(n * BPS) : 0u);
+        float2 v[PT];
+        if constexpr (STG) {
+            // every wave's piece of this item's frame has landed
+            if (pending >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else if (pending >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        // ---- pre-stage (DIF residue r) + step 1: v[t] = y[tid + 1024 t]
+        using RawT = typename Raw<FMT>::T;
+        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+            ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, false, 0, true>(v, a.window_il, a.wide_tw, in_rs, tq,
+                                                                             n * 4, reinterpret_cast<const RawT *>(buf))
+                      : void()), ...);
+        }(std::make_integer_sequence<int, RS>{});
+        dft<32>(v);  // z[k2], natural order
+        if constexpr (!(RFA_W64_ABL & 1)) {  // * W_M^(tid k2) = A[tid >> 5][k2] * B[tid & 31][k2] (exact tables)
+            const float2 *ra = tp2 + (tq >> 5) * G::P2_ROW - 1;
+            const float2 *rb = tp2 + G::TW_P2A + (tq & 31) * G::P2_ROW - 1;
+            v[1] = cmul(v[1], cmul(ra[1], rb[1]));
+#pragma unroll
+            for (int t = 2; t < 32; t += 2) {
+                float2 w0 = ra[t], w1 = ra[t + 1];
+                cmul2(w0, rb[t], w1, rb[t + 1]);
+                cmul2(v[t], w0, v[t + 1], w1);
+            }
+        }
+        // ---- exchange 0: buffer [k2][m1 - 512 h] per half-round h (m1 half), 16 K points
+        lds_barrier();  // the staged frame and every wave's previous transpose are consumed
+        // round 0 lands in tmp (v is still live in waves 8..15), round 1 straight in v
+        float2 tmp[16];
+        if constexpr (!(RFA_W64_ABL & 2)) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                if ((tid >> 9) == h) {  // wave-uniform: waves 8h .. 8h + 7 hold m1 in this half
+                    float2 *w = buf + (tq - 512 * h);
+#pragma unroll
+                    for (int k = 0; k < 32; k++) w[k * 512] = v[k];
+                }
+                lds_barrier();
+                const float2 *rd = buf + k2 * 512 + l32;
+#pragma unroll
+                for (int bb = 0; bb < 16; bb++) {  // m1 = l32 + 32 (16 h + bb)
+                    if (h == 0) tmp[bb] = rd[32 * bb];
+                    else v[16 + bb] = rd[32 * bb];
+                }
+                lds_barrier();
+            }
+#pragma unroll
+            for (int t = 0; t < 16; t++) v[t] = tmp[t];
+        }
+        // ---- step 2, pass A: DFT32 over b, then * W_1024^(a c) (a = l32; table row a)
+        dft<32>(v);
+        if constexpr (!(RFA_W64_ABL & 8)) {
+            const float2 *row = tp1 + l32 * G::P1_ROW - 1;
+            v[1] = cmul(v[1], row[1]);
+#pragma unroll
+            for (int t = 2; t < 32; t += 2) cmul2(v[t], row[t], v[t + 1], row[t + 1]);
+        }
+        // ---- transpose inside the wave, two rounds by a half (a = 16 ar + a'): the writers
+        // (lanes of that half, EXEC-masked) store T[a'][c] at a' * 33 + c, every lane c then
+        // reads its 16 values; the odd pitch keeps both directions conflict free and every
+        // address is a lane base plus an immediate
+        if constexpr (!(RFA_W64_ABL & 4)) {
+            float2 *tw = buf + wave * WREG + ((tq >> 5) & 1) * 528;
+#pragma unroll
+            for (int ar = 0; ar < 2; ar++) {
+                if ((l32 >> 4) == ar) {
+                    float2 *w = tw + (l32 - 16 * ar) * 33;
+#pragma unroll
+                    for (int c = 0; c < 32; c++) w[c] = v[c];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                const float2 *rd = tw + l32;
+#pragma unroll
+                for (int ap = 0; ap < 16; ap++) {
+                    if (ar == 0) tmp[ap] = rd[ap * 33];
+                    else v[16 + ap] = rd[ap * 33];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+#pragma unroll
+            for (int t = 0; t < 16; t++) v[t] = tmp[t];
+        }
+#ifdef RFA_W64_EARLY_DMA
+        // this wave's region is free: stage its piece of the next item's frame
+        {
+            const int un = u + (int)gridDim.x;
+            if (un < items && frame_of(un) < a.n_frames) stage_piece(frame_of(un));
+        }
+#endif
+        // ---- pass B: DFT32 over a -> v[d] = Y[k2 + 32 c + 1024 d], c = l32
+        dft<32>(v);
+        pending = 0;
+        // stage this wave's piece of the next item's frame into its (free) region now,
+        // behind the epilogue's stores' issue: no compiler-placed vmcnt wait of the
+        // epilogue can then end up waiting for the DMA (in issue order it is younger)
+        auto stage_next = [&]() {
+#ifndef RFA_W64_EARLY_DMA
+            const int un = u + (int)gridDim.x;
+            if (un < items && frame_of(un) < a.n_frames) stage_piece(frame_of(un));
+#endif
+        };
+        if (active) {
+        // ---- epilogue (nativedsp.cpp:73-78): bin K = r + 2 (k2 + 32 c + 1024 d); fft-shift
+        // (nativedsp.cpp:77) turns d into d' = (d + 16) mod 32: natural index r + 2 k2 + 64 c + 2048 d',
+        // ring element (r + 2 k2) * 1024 + c + 32 d' (ring_pos, logrs 6)
+        constexpr float db_off = -kDbPerLog2 * (float)(2 * 16);
+        const bool to_ring = a.ring && frame >= a.ring_first;
+        int rr = 0;
+        if (to_ring) {
+            rr = (a.ring_base - frame) % a.ring_rows;
+            if (rr < 0) rr += a.ring_rows;
+        }
+        const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n + r : nullptr, a.rows ? n * 4 : 0);
+        const rsrc_t ring_rs =
+            make_rsrc(to_ring ? a.ring + (size_t)rr * n + (size_t)r * 1024 : nullptr, to_ring ? n * 4 : 0);
+        const int vo_ring = (2 * k2 * 1024 + l32) * 4, vo_row = (2 * k2 + 64 * l32) * 4;
+        auto epilogue = [&](auto row_c, auto ring_c) {
+#pragma unroll
+            for (int d = 0; d < 32; d++) {
+                const int dp = (d + 16) & 31;
+                const float db = db_unscaled(v[d], db_off);
+                if constexpr (decltype(row_c)::value) buf_store_f32(db, row_rs, vo_row, 2048 * dp * 4);
+                if constexpr (decltype(ring_c)::value) buf_store_f32(db, ring_rs, vo_ring, 32 * dp * 4);
+            }
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        if constexpr (RFA_W64_ABL & 16) {
+            if (to_ring) epilogue(F_{}, T_{});
+        } else {
+            if (a.rows && to_ring) epilogue(T_{}, T_{});
+            else if (a.rows) epilogue(T_{}, F_{});
+            else if (to_ring) epilogue(F_{}, T_{});
+        }
+        }
+        stage_next();
+#ifdef RFA_W64_EARLY_DMA
+        pending = (a.rows ? 32 : 0) + (to_ring ? 32 : 0);
+#endif
+    }
+}
+
+template <int FMT, bool STG>
+static hipError_t launch_w64_one(const FftLaunch &a) {
+    using G = WGeo<15, 32>;
+    auto kern = &fft_w64_kernel<FMT, STG>;
+    const size_t lds = (size_t)G::LDS_BYTES;
+    if (!a.wide_tw || !a.window_il) return hipErrorInvalidValue;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int items = ((a.n_frames + 7) / 8) * 8 * 2;
+    if (items <= 0) return hipSuccess;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    // persistent: one 1024-thread workgroup per CU (LDS and registers), items strided by the grid
+    const int blocks = std::min(items, cus);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(1024), lds, a.stream, a);
+    return hipGetLastError();
+}
+
+static hipError_t launch_w64(const FftLaunch &a) {
+    const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
+    switch (a.fmt) {
+    case 0: return stg ? launch_w64_one<0, true>(a) : launch_w64_one<0, false>(a);
+    case 1: return stg ? launch_w64_one<1, true>(a) : launch_w64_one<1, false>(a);
+    case 2: return launch_w64_one<2, false>(a);
+    case 3: return launch_w64_one<3, false>(a);
+    case 4: return launch_w64_one<4, false>(a);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+int ring_logrs_for(int logn, int wide_big, int w64) {
+    if (!wide_supported(logn) || logn <= 14) return 0;
+    if (logn == 16 && wide_big == 15 && w64) return 6;
+    return logn - wide_logm(logn, wide_big);
+}
+
 template <int LOGM, int PT, int RS, bool CO>
 static hipError_t wide_by_fmt(const FftLaunch &a) {
     if constexpr (CO) {
@@ -824,7 +1105,9 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
     if (a.logn >= 15 && a.wide_big == 15) {
         switch (a.logn) {
         case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
-        case 16: return co ? wide_by_fmt<15, 32, 2, true>(a) : wide_by_fmt<15, 32, 2, false>(a);
+        case 16:
+            if (!co && a.w64) return launch_w64(a);
+            return co ? wide_by_fmt<15, 32, 2, true>(a) : wide_by_fmt<15, 32, 2, false>(a);
         case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
         default: return hipErrorInvalidValue;
         }

@@ -290,3 +290,27 @@ def test_fft_size_change_restarts_ring_and_peaks(rfa):
         assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL
         assert gu.db_diff(e.ema(), p.ema) <= gu.DB_TOL
         assert gu.db_diff(e.ema(), processor.ema_batch(rows_b, 0.25)) <= gu.DB_TOL
+
+
+def test_w64_wave_kernel_opt_in(rfa, monkeypatch):
+    """RFA_W64=1 selects the four-step wave kernel at N = 64 K (fft_wide.hip, opt-in):
+    ring order 64 (ring_pos logrs 6), rows / ring / peaks / EMA / boxcar equal the
+    restatement as with the default kernel."""
+    monkeypatch.setenv("RFA_W64", "1")
+    n, frames, rows_r = 65536, 40, 30
+    data, ref = _cfg3_rows(n, frames, 7)
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.1, peak_hold=True, ring_rows=rows_r) as e:
+        assert e.ring_order == 64
+        e.set_tuning(433_920_000, 20_000_000)
+        rows = e.process(data[: 10 * 2 * n], 10)           # caller rows (natural order) + ring
+        assert gu.db_diff(rows, ref[:10]) <= gu.DB_TOL
+        e.process(data[10 * 2 * n:], frames - 10, rows=False)  # ring only (the hot path)
+        assert gu.db_diff(e.peaks(), ref.max(0)) <= gu.DB_TOL
+        assert gu.db_diff(e.ema(), processor.ema_batch(ref, 0.1)) <= gu.DB_TOL
+        ring, ri, _ = e.ring()
+        newest = [(ri + k) % rows_r for k in range(rows_r)]
+        assert gu.db_diff(ring[newest], ref[::-1][:rows_r]) <= gu.DB_TOL
+        p = processor.FftProcessorRef(n, rows_r)
+        for r in ref:
+            p.push(r, 433_920_000, 20_000_000)
+        assert gu.db_diff(e.boxcar(3), p.boxcar(3)) <= gu.DB_TOL
