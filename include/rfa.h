@@ -177,9 +177,13 @@ RFA_API int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, si
 /* Display preprocessing: the reference's
  * AnalyzerSurface.drawPreprocessing (app/.../ui/AnalyzerSurface.kt:599-743)
  * computed on the device from the ring, for the tuning of rfa_set_tuning and the
- * newest row rfa_get_ring reports.  Every ring row is (re)computed (the
- * reference refreshes dirty rows lazily; the result equals its colour buffer
- * once every row has been refreshed).  Outputs (host, synchronous):
+ * newest row rfa_get_ring reports.  The handle keeps the draw thread's state:
+ * a persistent colour buffer and the dirty map (waterfallBufferDirtyMap).  Rows
+ * written by rfa_process are dirty; a retune, clear, ring resize, new width or
+ * new viewport / vertical scale marks every row.  A draw refreshes, newest
+ * first, every dirty row and rows 0..average_length, at most
+ * average_length + 6 rows (AnalyzerSurface.kt:619-640,678-684); the other rows
+ * keep their colours, exactly as in the reference.  Outputs (host, synchronous):
  *   colors      [ring_rows][width] ARGB, ring storage order (colorBuffer[bufferIndex*width + i]):
  *               colormap[clamp(((avg - min_db) * scale).toInt())] of the pixel's mean
  *               bin value, black (0xff000000) outside the drawn range;

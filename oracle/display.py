@@ -12,8 +12,12 @@ waterfall ring before drawing (paths relative to app/src/main/java/com/mantz_it/
   min / max (:663-665,713-718), the peak-hold y of row 0 (:707, -1 outside);
 * ``createGqrxMap`` (ui/ColorMaps.kt:41-51) for realistic colour maps.
 
-Every row is processed (the reference refreshes dirty rows lazily; a full
-refresh is what it converges to).  Pure-Python loops: small sizes only.
+``draw_preprocess`` processes every row (what the lazy refresh converges to);
+``Surface`` adds the reference's dirty-row bookkeeping (:619-640,678-684,735:
+rows written since the last draw, everything after a viewport / scale / size
+change, at most L + 6 rows per draw, the colour buffer persisting between draws)
+with the marks FftProcessor sets (analyzer/FftProcessor.kt:181,193,215,219,223).
+Pure-Python loops: small sizes only.
 """
 from __future__ import annotations
 
@@ -91,10 +95,12 @@ def _jmax(a: np.float32, b: np.float32) -> np.float32:
 
 def draw_preprocess(ring: np.ndarray, read_index: int, peaks, frequency: int, sample_rate: int, width: int,
                     fft_height: int, viewport_frequency: int, viewport_sample_rate: int, min_db: float, max_db: float,
-                    average_length: int, colormap: np.ndarray):
+                    average_length: int, colormap: np.ndarray, dirty=None, colors=None):
     """AnalyzerSurface.kt:599-743.  Returns (colors [R][width] uint32 in ring storage
     order, path_y [width] float32 (NaN: no path point), peaks_y [width] or None,
-    (autoscale_min, autoscale_max))."""
+    (autoscale_min, autoscale_max)).  With ``dirty`` (bool per ring row, updated in
+    place) and ``colors`` (the persistent colour buffer, updated in place) only the
+    rows the reference refreshes are processed (:678-684)."""
     R, fft_size = ring.shape
     ring = ring.astype(np.float32, copy=False)
     min_db, max_db = F32(min_db), F32(max_db)
@@ -114,13 +120,20 @@ def draw_preprocess(ring: np.ndarray, read_index: int, peaks, frequency: int, sa
     last_pixel = (kotlin_float_to_int(F32(fft_size - start) / samples_per_px) if end >= fft_size
                   else kotlin_float_to_int(F32(end - start) / samples_per_px))
 
-    colors = np.zeros((R, width), np.uint32)
+    if colors is None:
+        colors = np.zeros((R, width), np.uint32)
     time_avg = np.zeros(width, np.float32)
     path_y = np.full(width, np.nan, np.float32)
     peaks_y = np.zeros(width, np.float32) if peaks is not None else None
     mn, mx = VERTICAL_SCALE_UPPER_BOUNDARY, VERTICAL_SCALE_LOWER_BOUNDARY
+    rows_processed = 0
     for row_number in range(R):
         buffer_index = (read_index + row_number) % R
+        if dirty is not None:
+            if not dirty[buffer_index] and row_number > average_length:
+                continue  # already up to date
+            if rows_processed > average_length + 5:
+                break     # at most 5 dirty rows beyond the averaged ones per draw
         row = ring[buffer_index]
         for i in range(width):
             if first_pixel + 1 <= i < last_pixel - 1:
@@ -153,4 +166,41 @@ def draw_preprocess(ring: np.ndarray, read_index: int, peaks, frequency: int, sa
                 colors[buffer_index, i] = BLACK
                 if peaks is not None:
                     peaks_y[i] = F32(-1.0)
+        rows_processed += 1
+        if dirty is not None:
+            dirty[buffer_index] = False
     return colors, path_y, peaks_y, (float(mn), float(mx))
+
+
+class Surface:
+    """The draw thread's persistent state: colour buffer, dirty map, last viewport."""
+
+    def __init__(self, ring_rows: int):
+        self.dirty = np.ones(ring_rows, bool)
+        self.colors = None
+        self.last = None
+
+    def mark_row(self, buffer_index: int) -> None:  # FftProcessor.kt:223 (the row just written)
+        self.dirty[buffer_index] = True
+
+    def mark_all(self, ring_rows: int | None = None) -> None:  # :181,193,215,219 (new size, resize, retune)
+        if ring_rows is not None and ring_rows != self.dirty.size:
+            self.dirty = np.ones(ring_rows, bool)
+        self.dirty[:] = True
+
+    def draw(self, ring, read_index, peaks, frequency, sample_rate, width, fft_height, viewport_frequency,
+             viewport_sample_rate, min_db, max_db, average_length, colormap):
+        R = ring.shape[0]
+        if self.dirty.size != R:
+            self.mark_all(R)
+        if self.colors is None or self.colors.shape != (R, width):  # :619-626 new bitmap / colour buffer
+            self.colors = np.zeros((R, width), np.uint32)
+            self.dirty[:] = True
+        key = (viewport_frequency, viewport_sample_rate, F32(min_db), F32(max_db))
+        if key != self.last:  # :634-640
+            self.dirty[:] = True
+            self.last = key
+        c, p, k, mm = draw_preprocess(ring, read_index, peaks, frequency, sample_rate, width, fft_height,
+                                      viewport_frequency, viewport_sample_rate, min_db, max_db, average_length,
+                                      colormap, dirty=self.dirty, colors=self.colors)
+        return c.copy(), p, k, mm

@@ -43,11 +43,14 @@ __device__ __forceinline__ float jmax(float a, float b) {
     return a > b ? a : b;
 }
 
+// One block row per refreshed ring row (the host picks them as the reference's
+// dirty-row loop does, AnalyzerSurface.kt:678-684); the other rows keep their colours.
 __global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int row_number = blockIdx.y;
+    const int2 sel = a.rows[blockIdx.y];
+    const int row_number = sel.x;
     if (i >= a.width) return;
-    const int buffer_index = (a.read_index + row_number) % a.ring_rows;
+    const int buffer_index = sel.y;
     const float *row = a.ring + (size_t)buffer_index * a.n;
     const int lm = (31 - __clz(a.n)) - a.ring_logrs;  // ring storage order (ring_pos)
     unsigned *out = a.colors + (size_t)buffer_index * a.width + i;
@@ -168,8 +171,8 @@ hipError_t launch_row_windows(const float *row, int ring_logrs, int n, const int
 }
 
 hipError_t launch_draw(const DrawLaunch &a) {
-    if (a.width <= 0 || a.ring_rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(draw_rows_kernel, dim3((a.width + 255) / 256, a.ring_rows), dim3(256), 0, a.stream, a);
+    if (a.width <= 0 || a.ring_rows <= 0 || a.n_rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(draw_rows_kernel, dim3((a.width + 255) / 256, a.n_rows), dim3(256), 0, a.stream, a);
     hipLaunchKernelGGL(draw_finish_kernel, dim3(1), dim3(1024), 0, a.stream, a);
     return hipGetLastError();
 }

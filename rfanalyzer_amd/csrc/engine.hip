@@ -73,8 +73,16 @@ struct rfa_handle {
     int64_t chan_start = 0, chan_end = 0;
     float *d_chan = nullptr;
     size_t d_chan_cap = 0;
-    void *d_draw = nullptr;           // rfa_draw_preprocess: colormap, colours, averages, outputs
+    void *d_draw = nullptr;           // rfa_draw_preprocess: colormap, averages, outputs, row list
     size_t d_draw_cap = 0;
+    // the draw thread's persistent state (AnalyzerSurface.kt:619-640,678-684,735):
+    // colour buffer, dirty map (FftProcessorData.waterfallBufferDirtyMap), last viewport
+    unsigned *d_colors = nullptr;
+    int colors_rows = 0, colors_width = 0;
+    std::vector<uint8_t> dirty;
+    bool have_view = false;
+    int64_t view_frequency = 0, view_sample_rate = 0;
+    float view_min_db = 0.f, view_max_db = 0.f;
     size_t chan_count = 0;
     int64_t last_frequency = 0, last_sample_rate = 0;
     // staging for host-pointer entry points / state without a row buffer
@@ -319,6 +327,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
 }
 
 int clear_ring(rfa_handle *h) {
+    std::fill(h->dirty.begin(), h->dirty.end(), 1);  // FftProcessor.kt:215,219
     if (!h->d_ring) return RFA_OK;
     HIPCHK(h, rfa::launch_fill(h->d_ring, (long long)h->ring_rows * h->n, kRingFill, h->stream));
     return RFA_OK;
@@ -504,6 +513,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (hipMemcpy(h->d_twc, tc.data(), nc * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
     if (hipMemcpy(h->d_twf, tf.data(), nf * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
     // state
+    h->dirty.assign((size_t)std::max(h->ring_rows, 0), 1);  // FftProcessor.kt:181
     if (h->ring_rows > 0) {
         const size_t bytes = (size_t)h->ring_rows * n * sizeof(float);
         if (hipMalloc(&h->d_ring, bytes) != hipSuccess) return bail(RFA_ERR_NOMEM);
@@ -554,6 +564,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_state_part);
     hipFree(h->d_chan);
     hipFree(h->d_draw);
+    hipFree(h->d_colors);
     hipFree(h->d_boxcar);
     hipFree(h->d_in);
     hipFree(h->d_rows);
@@ -623,6 +634,7 @@ static int apply_ring_resize(rfa_handle *h) {
     h->d_ring_tmp = nt;
     h->ring_rows = rn;
     h->cfg.ring_rows = rn;
+    h->dirty.assign((size_t)rn, 1);  // FftProcessor.kt:193
     h->write_index = 0;
     if (h->read_index >= rn) h->read_index = 0;  // rewritten by the frame that triggered the resize
     return RFA_OK;
@@ -719,6 +731,9 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     if (h->d_ring) {
         const long long R = h->ring_rows;
         const long long last = (long long)n_frames - 1;
+        // the rows this batch wrote are dirty for the draw thread (FftProcessor.kt:223)
+        for (long long f = std::max<long long>(0, (long long)n_frames - R); f < (long long)n_frames; f++)
+            h->dirty[(size_t)((((long long)h->write_index - f) % R + R) % R)] = 1;
         h->read_index = (int)((((long long)h->write_index - last) % R + R) % R);
         h->write_index = h->read_index == 0 ? h->ring_rows - 1 : h->read_index - 1;  // FftProcessor.kt:226-227
     }
@@ -793,6 +808,7 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
                 HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, h->ring_logrs, (int)off, kRingFill,
                                                  h->stream));
                 std::swap(h->d_ring, h->d_ring_tmp);
+                std::fill(h->dirty.begin(), h->dirty.end(), 1);  // FftProcessor.kt:215
             } else {
                 rc = clear_ring(h);
                 if (rc) return rc;
@@ -850,21 +866,54 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
     a.fft_height = p->fft_height;
     a.avg_length = L;
     a.colormap_size = p->colormap_size;
-    // one device block: colormap | colours [R][W] | averages [L+1][W] | path y | peaks y | autoscale
+    // persistent colour buffer (AnalyzerSurface.kt:619-626: a new size starts zeroed, all rows dirty)
+    if (!h->d_colors || h->colors_rows != R || h->colors_width != W) {
+        hipFree(h->d_colors);
+        h->d_colors = nullptr;
+        if (hipMalloc(&h->d_colors, (size_t)R * W * 4) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "colour buffer");
+        HIPCHK(h, hipMemsetAsync(h->d_colors, 0, (size_t)R * W * 4, h->stream));
+        h->colors_rows = R;
+        h->colors_width = W;
+        std::fill(h->dirty.begin(), h->dirty.end(), 1);
+    }
+    // a new viewport or vertical scale repaints everything (:634-640)
+    if (!h->have_view || p->viewport_frequency != h->view_frequency || p->viewport_sample_rate != h->view_sample_rate ||
+        p->min_db != h->view_min_db || p->max_db != h->view_max_db) {
+        std::fill(h->dirty.begin(), h->dirty.end(), 1);
+        h->have_view = true;
+        h->view_frequency = p->viewport_frequency;
+        h->view_sample_rate = p->viewport_sample_rate;
+        h->view_min_db = p->min_db;
+        h->view_max_db = p->max_db;
+    }
+    // the rows this draw refreshes, newest first (:678-684): every dirty row and rows
+    // 0..L (the time average), at most L + 6 of them; refreshed rows become clean
+    std::vector<int2> sel;
+    for (int row_number = 0; row_number < R; row_number++) {
+        const int bi = (h->read_index + row_number) % R;
+        if (!h->dirty[bi] && row_number > L) continue;
+        if ((int)sel.size() > L + 5) break;
+        sel.push_back(make_int2(row_number, bi));
+        h->dirty[bi] = 0;
+    }
+    // one device block: colormap | row list | averages [L+1][W] | path y | peaks y | autoscale
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t b_cmap = al((size_t)p->colormap_size * 4), b_col = al((size_t)R * W * 4),
+    const size_t b_cmap = al((size_t)p->colormap_size * 4), b_sel = al(sel.size() * sizeof(int2)),
                  b_avg = al((size_t)(L + 1) * W * 4), b_w = al((size_t)W * 4);
-    rc = ensure_device_buffer(h, &h->d_draw, &h->d_draw_cap, b_cmap + b_col + b_avg + 2 * b_w + 256);
+    rc = ensure_device_buffer(h, &h->d_draw, &h->d_draw_cap, b_cmap + b_sel + b_avg + 2 * b_w + 256);
     if (rc) return rc;
-    char *base = static_cast<char *>(h->d_draw);
+    char *base = static_cast<char *>(h->d_draw) + b_sel;
     a.colormap = reinterpret_cast<const unsigned *>(base);
-    a.colors = reinterpret_cast<unsigned *>(base + b_cmap);
-    a.avg_rows = reinterpret_cast<float *>(base + b_cmap + b_col);
-    a.path_y = reinterpret_cast<float *>(base + b_cmap + b_col + b_avg);
-    a.peaks_y = peaks_y ? reinterpret_cast<float *>(base + b_cmap + b_col + b_avg + b_w) : nullptr;
-    a.autoscale = reinterpret_cast<float *>(base + b_cmap + b_col + b_avg + 2 * b_w);
+    a.rows = reinterpret_cast<const int2 *>(static_cast<char *>(h->d_draw));
+    a.n_rows = (int)sel.size();
+    a.colors = h->d_colors;
+    a.avg_rows = reinterpret_cast<float *>(base + b_cmap);
+    a.path_y = reinterpret_cast<float *>(base + b_cmap + b_avg);
+    a.peaks_y = peaks_y ? reinterpret_cast<float *>(base + b_cmap + b_avg + b_w) : nullptr;
+    a.autoscale = reinterpret_cast<float *>(base + b_cmap + b_avg + 2 * b_w);
     a.stream = h->stream;
     HIPCHK(h, hipMemcpyAsync(base, p->colormap, (size_t)p->colormap_size * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_draw, sel.data(), sel.size() * sizeof(int2), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, rfa::launch_draw(a));
     HIPCHK(h, hipMemcpyAsync(colors, a.colors, (size_t)R * W * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipMemcpyAsync(fft_path_y, a.path_y, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));

@@ -145,7 +145,9 @@ struct DrawLaunch {
     float samples_per_px = 0.f, min_db = 0.f, db_width = 0.f, scale = 0.f;
     const unsigned *colormap = nullptr;
     int colormap_size = 0;
-    unsigned *colors = nullptr;    // [ring_rows][width], ring storage order
+    unsigned *colors = nullptr;    // [ring_rows][width], ring storage order (persistent between draws)
+    const int2 *rows = nullptr;    // the rows to refresh this draw: (rowNumber, bufferIndex), newest first
+    int n_rows = 0;
     float *avg_rows = nullptr;     // scratch [avg_length + 1][width]
     float *path_y = nullptr;       // [width]
     float *peaks_y = nullptr;      // [width] or null

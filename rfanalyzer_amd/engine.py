@@ -227,7 +227,9 @@ class SpectrumEngine:
                         min_db: float, max_db: float, average_length: int, colormap, peaks: bool = False):
         """AnalyzerSurface.drawPreprocessing (AnalyzerSurface.kt:599-743) on the device, from the ring.
 
-        Returns (colors [ring_rows][width] uint32 ARGB in ring storage order,
+        Like the reference's draw thread it refreshes only dirty rows plus the
+        averaged ones (at most average_length + 6 per call, :678-684) and keeps
+        the colour buffer between calls.  Returns (colors [ring_rows][width] uint32 ARGB in ring storage order,
         fft_path_y [width] (NaN where no path point), peaks_y [width] or None,
         (autoscale_min, autoscale_max))."""
         self._sync_config()

@@ -71,3 +71,31 @@ def test_no_valid_pixels_gives_initial_autoscale():
     colors, path, _, mm = _draw(ring, viewport_frequency=100_000_000 + 10_000_000)  # far outside the data
     assert (colors == od.BLACK).all() and np.isnan(path).all()
     assert mm == (10.0, -100.0)
+
+
+def test_surface_dirty_rows_converge():
+    """od.Surface (the reference's dirty-row bookkeeping, AnalyzerSurface.kt:619-640,
+    678-684): a first draw of R > L + 6 rows refreshes L + 6 of them, newest first;
+    the next draw refreshes the rest; then it equals the full refresh."""
+    rng = np.random.default_rng(9)
+    R2 = 12
+    ring = rng.uniform(-90, -10, (R2, N)).astype(np.float32)
+    args = dict(read_index=5, peaks=None, frequency=100_000_000, sample_rate=2_000_000, width=W, fft_height=400,
+                viewport_frequency=100_000_000, viewport_sample_rate=2_000_000, min_db=-80.0, max_db=0.0,
+                average_length=2, colormap=od.gqrx_colormap())
+    surf = od.Surface(R2)
+    c1 = surf.draw(ring, **args)[0]
+    done = [(5 + j) % R2 for j in range(2 + 6)]
+    assert (c1[done] != 0).any(axis=1).all()
+    assert (c1[[r for r in range(R2) if r not in done]] == 0).all()
+    c2, p2, _, mm2 = surf.draw(ring, **args)
+    full = od.draw_preprocess(ring, **args)
+    np.testing.assert_array_equal(c2, full[0])
+    np.testing.assert_array_equal(p2, full[1])
+    assert mm2 == full[3]
+    # a row changed without a dirty mark keeps its old colours (the reference's lazy refresh)
+    ring2 = ring.copy()
+    ring2[(5 + 9) % R2] = -5.0
+    np.testing.assert_array_equal(surf.draw(ring2, **args)[0], c2)
+    surf.mark_row((5 + 9) % R2)
+    np.testing.assert_array_equal(surf.draw(ring2, **args)[0], od.draw_preprocess(ring2, **args)[0])

@@ -21,13 +21,16 @@ def _engine(rfa, frames, n=N):
     return e
 
 
-def _both(e, **kw):
+def _both(e, surf=None, tuning=(F0, SR), **kw):
+    """One draw on the device and on the restated draw thread (od.Surface: the
+    persistent colour buffer and dirty map, AnalyzerSurface.kt:619-640,678-684)."""
     ring, ri, _ = e.ring()
     args = dict(width=333, fft_height=480, viewport_frequency=F0, viewport_sample_rate=SR, min_db=-110.0,
                 max_db=-20.0, average_length=3, colormap=od.gqrx_colormap())
     args.update(kw)
     got = e.draw_preprocess(peaks=True, **args)
-    exp = od.draw_preprocess(ring, ri, e.peaks(), F0, SR, **args)
+    surf = surf or od.Surface(ring.shape[0])
+    exp = surf.draw(ring, ri, e.peaks(), *tuning, **args)
     return got, exp
 
 
@@ -53,9 +56,10 @@ def test_viewports_bit_exact(rfa, vf, vsr):
 
 def test_partial_ring_and_no_average(rfa):
     e = _engine(rfa, 5)  # rows 5..11 still hold the -9999 fill
+    surf = od.Surface(R)
     try:
-        _assert_same(*_both(e, average_length=0, width=1000))
-        _assert_same(*_both(e, average_length=R - 1, min_db=-150.0, max_db=0.0))
+        _assert_same(*_both(e, surf, average_length=0, width=1000))  # 6 of 12 rows refreshed
+        _assert_same(*_both(e, surf, average_length=R - 1, min_db=-150.0, max_db=0.0))
     finally:
         e.close()
 
@@ -69,6 +73,47 @@ def test_residue_major_ring_bit_exact(rfa, n):
     try:
         assert e.ring_order == {65536: 2, 131072: 4}[n]
         _assert_same(*_both(e, width=1111, viewport_frequency=F0 + 150_000, viewport_sample_rate=SR // 3))
+    finally:
+        e.close()
+
+
+def test_dirty_rows_across_draws(rfa):
+    """The reference refreshes only dirty rows plus the L + 1 averaged ones, at most
+    L + 6 rows per draw (AnalyzerSurface.kt:678-684); FftProcessor marks the rows it
+    writes (FftProcessor.kt:223) and everything on a resize / retune (:181,193,215,219).
+    The device keeps the same colour buffer and dirty map: a sequence of draws
+    interleaved with new frames, a retune shift, a clear and a viewport change stays
+    bit-identical to the restated draw thread, including the rows still pending."""
+    n = 2048
+    e = rfa.SpectrumEngine(n, "blackman", "s8", avg="none", peak_hold=True, ring_rows=R)
+    e.set_tuning(F0, SR)
+    surf = od.Surface(R)
+    seed = [30]
+
+    def feed(k):
+        seed[0] += 1
+        e.process(signals.frames_bytes(n, k, "s8", seed=seed[0], tones=((0.13, 0.4),), noise=0.05), k, rows=False)
+        ri = e.ring()[1]
+        for j in range(min(k, R)):
+            surf.mark_row((ri + j) % R)
+
+    try:
+        feed(20)
+        for step in range(4):  # R = 12 > L + 6 = 9: the first draws converge over two calls
+            _assert_same(*_both(e, surf))
+            feed(step + 1)
+        _assert_same(*_both(e, surf))
+        _assert_same(*_both(e, surf))  # nothing new: only the averaged rows are redrawn
+        e.set_tuning(F0 + 10_000, SR)  # shift by a few bins: every row dirty
+        surf.mark_all()
+        t = (F0 + 10_000, SR)
+        _assert_same(*_both(e, surf, t))
+        feed(2)
+        _assert_same(*_both(e, surf, t, viewport_frequency=F0 + 50_000))  # new viewport: all dirty
+        _assert_same(*_both(e, surf, t, viewport_frequency=F0 + 50_000))
+        e.set_tuning(F0, 2 * SR)  # sample-rate change clears the ring
+        surf.mark_all()
+        _assert_same(*_both(e, surf, (F0, 2 * SR), width=500))  # new width: new colour buffer
     finally:
         e.close()
 
