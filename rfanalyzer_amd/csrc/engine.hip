@@ -34,12 +34,12 @@ struct rfa_handle {
     float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
     float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
     float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17, and kernel A for larger N)
-    // N = 2^18..2^20 (decimation in time, fft_large.hip)
-    float *d_dit_window = nullptr;    // scaled window permuted to [S][M]: w[S m + r] at [r][m]
-    float *d_dit_black = nullptr;     // unscaled Blackman, same permutation (NativeDsp.kt seam)
-    float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{r k} = C[r][k >> 7] * D[r][k & 127]
-    float2 *d_dit_y = nullptr;        // scratch [frames][S][M] complex
+    // N = 2^18..2^20 (decimation in frequency, fft_large.hip)
+    float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{m s} = C[s][m >> 7] * D[s][m & 127]
+    float2 *d_dit_y = nullptr;        // scratch z [frames][S][M] complex
     size_t d_dit_y_cap = 0;
+    float *d_dit_db = nullptr;        // caller rows of a batch, residue-major, before cols_to_rows
+    size_t d_dit_db_cap = 0;
     int dit_frames = 1;               // frames per kernel-A/B pair (scratch <= kDitScratch)
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
@@ -218,43 +218,48 @@ hipEvent_t get_event(rfa_handle *h) {
     return e;
 }
 
-// N = 2^18..2^20: kernel A (wide kernel on the S strided sub-frames, complex out
-// to scratch) + kernel B (radix-S combine, dB rows / ring / complex out), in
+// N = 2^18..2^20: kernel A (column DFT-S + twiddle, complex scratch z) + kernel B
+// (the 32 K-point wide kernel on each z_s: dB rows / ring / complex out), in
 // batches of dit_frames frames so the scratch stays cache resident.
 static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
     const int n = h->n, s = n >> rfa::kDitLogM;
-    const float *win = a.window == h->d_window         ? h->d_dit_window
-                       : a.window == h->d_window_black ? h->d_dit_black
-                                                       : a.window;  // all-ones table: any layout
     for (int f0 = 0; f0 < a.n_frames; f0 += h->dit_frames) {
         const int cnt = std::min(h->dit_frames, a.n_frames - f0);
-        FftLaunch A = a;
+        rfa::DifLaunch A;
         A.in = a.in + (size_t)f0 * (size_t)a.frame_stride;
+        A.frame_stride = a.frame_stride;
         A.n_frames = cnt;
-        A.dit_ss = s;
-        A.window = win;
-        A.rows = nullptr;
-        A.ring = nullptr;
-        A.complex_out = h->d_dit_y;
-        hipError_t e = rfa::launch_fft_wide(A);
+        A.fmt = a.fmt;
+        A.logn = h->logn;
+        A.window = a.window;  // natural order: the scaled window or a seam window
+        A.tw_c = h->d_dit_c;
+        A.tw_d = h->d_dit_d;
+        A.z = h->d_dit_y;
+        A.stream = a.stream;
+        hipError_t e = rfa::launch_dif_front(A);
         if (e != hipSuccess) return e;
-        rfa::DitLaunch B;
-        B.y = h->d_dit_y;
+        FftLaunch B = a;
+        B.in = reinterpret_cast<const uint8_t *>(h->d_dit_y);
+        B.frame_stride = (long long)n * (long long)sizeof(float2);
         B.n_frames = cnt;
-        B.frame0 = f0;
-        B.logn = h->logn;
-        B.logm = rfa::kDitLogM;
-        B.tw_c = h->d_dit_c;
-        B.tw_d = h->d_dit_d;
-        B.rows = a.rows ? a.rows + (size_t)f0 * n : nullptr;
-        B.ring = a.ring;
-        B.ring_rows = a.ring_rows;
-        B.ring_base = a.ring_base;
-        B.ring_first = a.ring_first;
+        B.fmt = rfa::kFmtDif;
+        B.dif_ss = s;
+        B.window = nullptr;
+        B.window_il = nullptr;
+        B.rows = a.rows ? h->d_dit_db : nullptr;
         B.complex_out = a.complex_out ? a.complex_out + (size_t)f0 * n : nullptr;
-        B.stream = a.stream;
-        e = rfa::launch_dit_combine(B);
+        B.ring_base = a.ring_base - f0;  // frame f0 + f of the call is frame f of this pair
+        B.ring_first = a.ring_first - f0;
+        B.persist = 0;
+        B.stage = 0;
+        B.diag = 0;
+        B.stamps = nullptr;
+        e = rfa::launch_fft_wide(B);
         if (e != hipSuccess) return e;
+        if (a.rows) {
+            e = rfa::launch_cols_to_rows(h->d_dit_db, a.rows + (size_t)f0 * n, cnt, h->logn, a.stream);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipSuccess;
 }
@@ -282,7 +287,8 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     if (a.window == h->d_window) a.window_il = h->d_window_il;
     else if (h->logn > 14) a.variant = 1;  // seam windows have no interleaved copy: narrow kernel
     // the ring order is a property of the wide kernel's residue split (ring_pos)
-    if (a.ring && h->ring_logrs && a.variant == 1) return fail(h, RFA_ERR_INVALID, "ring order needs the wide kernel");
+    if (a.ring && h->ring_logrs && a.variant == 1 && h->logn <= 17)
+        return fail(h, RFA_ERR_INVALID, "ring order needs the wide kernel");
     a.max_logm = h->max_logm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->profile) {
@@ -302,6 +308,13 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
             h->d_dit_y_cap = 0;
             if (hipMalloc(&h->d_dit_y, need) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "large-N scratch");
             h->d_dit_y_cap = need;
+        }
+        if (a.rows && need / 2 > h->d_dit_db_cap) {
+            hipFree(h->d_dit_db);
+            h->d_dit_db = nullptr;
+            h->d_dit_db_cap = 0;
+            if (hipMalloc(&h->d_dit_db, need / 2) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "large-N row scratch");
+            h->d_dit_db_cap = need / 2;
         }
         e = launch_large(h, a);
     } else {
@@ -435,19 +448,10 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
     }
-    if (logn > 17) {  // decimation in time: S strided sub-frames of M = 32768 points
-        const int m = 1 << rfa::kDitLogM, s = n / m;
-        std::vector<float> pw(n), pb(n);
-        for (int r = 0; r < s; r++)
-            for (int i = 0; i < m; i++) {
-                pw[(size_t)r * m + i] = w[(size_t)s * i + r];
-                pb[(size_t)r * m + i] = black[(size_t)s * i + r];
-            }
+    if (logn > 17) {  // decimation in frequency: S column DFTs, then S sub-FFTs of M = 32768 points
         std::vector<float2> c, d, blob = rfa::wide_twiddles(rfa::kDitLogM, rfa::kWidePT, rfa::kDitLogM);
-        rfa::dit_twiddles(logn, c, d);
+        rfa::dif_twiddles(logn, c, d);
         struct { void **dst; const void *src; size_t bytes; } up[] = {
-            {(void **)&h->d_dit_window, pw.data(), pw.size() * sizeof(float)},
-            {(void **)&h->d_dit_black, pb.data(), pb.size() * sizeof(float)},
             {(void **)&h->d_dit_c, c.data(), c.size() * sizeof(float2)},
             {(void **)&h->d_dit_d, d.data(), d.size() * sizeof(float2)},
             {(void **)&h->d_wide_tw, blob.data(), blob.size() * sizeof(float2)}};
@@ -494,6 +498,9 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         else h->ring_logrs = rfa::ring_logrs_for(logn, h->wide_big, h->w64);
     } else {
         h->w64 = 0;
+        const char *nat = std::getenv("RFA_RING_NATURAL");
+        if (logn > 17 && !(nat && std::atoi(nat) != 0))  // large-N kernel B: ring block s holds bins S q + s
+            h->ring_logrs = rfa::ring_logrs_for(logn, h->wide_big, 0);
     }
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
@@ -550,11 +557,10 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_window_black);
     hipFree(h->d_window_il);
     hipFree(h->d_wide_tw);
-    hipFree(h->d_dit_window);
-    hipFree(h->d_dit_black);
     hipFree(h->d_dit_c);
     hipFree(h->d_dit_d);
     hipFree(h->d_dit_y);
+    hipFree(h->d_dit_db);
     hipFree(h->d_twc);
     hipFree(h->d_twf);
     hipFree(h->d_ring);

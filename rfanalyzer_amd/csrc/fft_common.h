@@ -390,7 +390,7 @@ template <int FMT>
 __device__ __forceinline__ typename Raw<FMT>::T buf_load_raw(rsrc_t rs, int voff, int soff, int planar_im_off) {
     if constexpr (FMT == 0 || FMT == 1) return (unsigned short)__builtin_amdgcn_raw_buffer_load_b16(rs, voff, soff, 0);
     else if constexpr (FMT == 2) return (unsigned)__builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0);
-    else if constexpr (FMT == 3) {
+    else if constexpr (FMT == 3 || FMT == 5) {  // f32 interleaved; 5: the large-N scratch
         return buf_load_f32x2(rs, voff, soff);
     } else {
         const float re = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, 0));

@@ -54,10 +54,11 @@ struct FftLaunch {
     int ring_first = 0;         // first frame that is stored into the ring
     int ring_logrs = 0;         // ring row order (ring_pos); must equal the kernel's residue split or 0
     float2 *complex_out = nullptr;  // ordered unscaled FFT (n_frames * N complex) instead of dB
-    // decimation in time for N > 2^17 (wide kernel, complex out): with dit_ss = S > 1
-    // work item u is sub-frame (frame u / S, residue u % S) = samples S*m + u % S of a
-    // frame of S*M samples; window points at the [S][M] permuted window
-    int dit_ss = 0;
+    // kernel B of the large-N pair (fmt == kFmtDif): S = dif_ss column residues per
+    // frame; work item u is (frame u / S, residue s = u % S), input z_s at
+    // in + (u * M) complex, outputs bins S q + s of an N = S * M frame; its dB rows
+    // target is residue-major (block s), like the ring
+    int dif_ss = 0;
     int wide_big = 15;        // wide_logm() for N > 16 K (RFA_WIDE_LOGM)
     int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
     long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
@@ -87,28 +88,30 @@ inline int wide_logm(int logn, int big) { return logn <= 14 ? logn : big; }
 std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
 
-// N = 2^18 .. 2^20: decimation-in-time pair (DESIGN.md "Large N").  Kernel A is
-// the wide kernel on the S = N / 32768 strided sub-frames of each frame (complex
-// out to scratch); kernel B (dit_combine_kernel) forms
-// X[k + M s] = sum_r W_N^{r k} Y_r[k] W_S^{r s} per k and writes dB rows / ring
-// (or the ordered complex spectrum).
-struct DitLaunch {
-    const float2 *y = nullptr;   // scratch [n_frames][S][M]
+// N = 2^18 .. 2^20: decimation-in-frequency pair (DESIGN.md "Large N", fft_large.hip).
+// Kernel A (dif_front_kernel) converts and windows the S = N / 32768 columns
+// x[m + M j] of each frame, DFT-S over j, twiddle W_N^{m s}, and writes scratch
+// z[f][s][m]; kernel B is the wide kernel on input format kFmtDif: the 32 K-point
+// FFT of each z_s gives bins S q + s (ring block s in residue-major order).
+struct DifLaunch {
+    const uint8_t *in = nullptr;   // raw frames, frame f at in + f * frame_stride
+    long long frame_stride = 0;
     int n_frames = 0;
-    int frame0 = 0;              // batch index of frame 0 (ring placement)
-    int logn = 0, logm = 15;
-    const float2 *tw_c = nullptr;  // [S][M/128]  W_N^{r * 128 * khi}
-    const float2 *tw_d = nullptr;  // [S][128]    W_N^{r * klo}
-    float *rows = nullptr;
-    float *ring = nullptr;
-    int ring_rows = 0, ring_base = 0, ring_first = 0;
-    float2 *complex_out = nullptr;
+    int fmt = 0;
+    int logn = 0;
+    const float *window = nullptr;  // natural order, N floats (scaled or seam window)
+    const float2 *tw_c = nullptr;   // [S][M/128]  W_N^{s * 128 * mhi}
+    const float2 *tw_d = nullptr;   // [S][128]    W_N^{s * mlo} - 1
+    float2 *z = nullptr;            // scratch [n_frames][S][M]
     hipStream_t stream = nullptr;
 };
 constexpr int kDitLogM = 15;
 constexpr int kMaxLogN = 20;
-hipError_t launch_dit_combine(const DitLaunch &a);
-void dit_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d);
+constexpr int kFmtDif = 5;  // wide-kernel input: kernel A's scratch (complex f32, already windowed)
+hipError_t launch_dif_front(const DifLaunch &a);
+// kernel B's residue-major dB rows -> natural order (caller rows of the large-N pair)
+hipError_t launch_cols_to_rows(const float *cols, float *rows, int n_frames, int logn, hipStream_t st);
+void dif_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at
 // rows + f*row_stride, or, when ring_rows > 0, at rows + ((ring_base - f) mod ring_rows)*n

@@ -1,16 +1,23 @@
-// N = 2^18 .. 2^20 (BASELINE config 5, 1 M-point FFT): decimation in time over
-// S = N / M sub-frames, M = 32768.
+// N = 2^18 .. 2^20 (BASELINE config 5, 1 M-point FFT): decimation in frequency
+// over S = N / M column DFTs, M = 32768.  With n = m + M j (m < M, j < S) and
+// k = S q + s (q < M, s < S):
 //
-// Kernel A (fft_wide.hip, dit_ss = S): sub-frame (f, r) = samples x_f[S m + r],
-// m < M, is converted, windowed (w[S m + r], the [S][M] permuted window) and
-// transformed by the 32 K-point workgroup: Y_r[k] = sum_m x[S m + r] w W_M^{m k},
-// written unscaled to scratch [f][r][k].
+//   X[S q + s] = sum_m W_M^{m q} [ W_N^{m s} sum_j x[m + M j] w[m + M j] W_S^{j s} ]
+//                                 `------------------ z_s[m] -------------------'
 //
-// Kernel B (here): X[k + M s] = sum_r (W_N^{r k} Y_r[k]) W_S^{r s}.  One thread
-// per k: S coalesced loads (consecutive k across lanes), exact twiddles
-// W_N^{r k} = C[r][k >> 7] * D[r][k & 127] (both from double), an in-register
-// DFT-S, then the reference's epilogue (nativedsp.cpp:72-79: 10*log10 of
-// |X|/N, fft-shift) -- every store is coalesced across lanes (k consecutive).
+// Kernel A (here, dif_front_kernel): one thread per m.  The S samples x[m + M j]
+// of a column sit in S contiguous rows of the frame, so every load instruction
+// is a run of consecutive samples across the lanes; convert (LUT-exact), window
+// (fp32 multiply with the natural window, NativeDsp.kt:55-58), an in-register
+// DFT-S, the twiddle W_N^{m s} = C[s][m >> 7] * (1 + D[s][m & 127]) (both tables
+// from double; D is the small difference to 1, so the product is nearly as exact
+// as C itself), and one coalesced 8-B store per s into scratch z[f][s][m].
+//
+// Kernel B (fft_wide.hip, input format 5): the 32 K-point workgroup transforms
+// z_s (contiguous, already windowed) and writes bins S q + s: into the device
+// ring as residue-major block s (ring_pos, logrs = log2 S -- whole lines per
+// workgroup); caller rows go residue-major to a scratch and cols_to_rows_kernel
+// puts them in natural order; the ordered complex spectrum is stored at stride S.
 // Scratch traffic is 16 B per sample (write + read); the engine sizes batches so
 // the scratch stays in the 256 MB Infinity Cache.
 #include <hip/hip_runtime.h>
@@ -23,55 +30,76 @@
 
 namespace rfa {
 
-template <int S, bool CO>
-__global__ void __launch_bounds__(256) dit_combine_kernel(DitLaunch a) {
-    const int M = 1 << a.logm, n = 1 << a.logn;
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+template <int S, int FMT>
+__global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
+    constexpr int M = 1 << kDitLogM, n = S * M;
+    constexpr int SB = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 || FMT == 4) ? 4 : 8;  // bytes per sample (per plane)
+    const int m = blockIdx.x * 256 + threadIdx.x;
     const int f = blockIdx.y;
-    if (k >= M) return;
-    const float2 *y = a.y + (size_t)f * S * M + k;
+    const rsrc_t in_rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * (FMT == 4 ? 8 : SB));
+    const rsrc_t w_rs = make_rsrc(a.window, n * 4);
+    // samples and window values in chunks of 8 rows, each chunk converted as it lands
+    // (fewer live registers than all raw values first: more waves per SIMD)
     float2 v[S];
+    constexpr int CH = S < 8 ? S : 8;
 #pragma unroll
-    for (int r = 0; r < S; r++) v[r] = y[(size_t)r * M];
-    const int khi = k >> 7, klo = k & 127, mc = M >> 7;
+    for (int j0 = 0; j0 < S; j0 += CH) {
+        typename Raw<FMT>::T raw[CH];
+        float w[CH];
 #pragma unroll
-    for (int r = 1; r < S; r++) v[r] = cmul(v[r], cmul(a.tw_c[r * mc + khi], a.tw_d[r * 128 + klo]));
-    dft<S>(v);  // v[s] = X[k + M s]
-    if constexpr (CO) {
-        float2 *o = a.complex_out + (size_t)f * n + k;
-#pragma unroll
-        for (int s = 0; s < S; s++) o[(size_t)s * M] = v[s];
-    } else {
-        const int frame = a.frame0 + f;
-        float *row = a.rows ? a.rows + (size_t)f * n : nullptr;
-        float *ring = nullptr;
-        if (a.ring && frame >= a.ring_first) {
-            int rr = (a.ring_base - frame) % a.ring_rows;
-            if (rr < 0) rr += a.ring_rows;
-            ring = a.ring + (size_t)rr * n;
+        for (int j = 0; j < CH; j++) {
+            raw[j] = buf_load_raw<FMT>(in_rs, m * SB, (j0 + j) * M * SB, n * 4);
+            w[j] = buf_load_f32(w_rs, m * 4, (j0 + j) * M * 4);
         }
-        const float db_off = db_offset(a.logn);
 #pragma unroll
-        for (int s = 0; s < S; s++) {
-            const float db = db_unscaled(v[s], db_off);      // nativedsp.cpp:73-78
-            const int o = (k + M * s + (n >> 1)) & (n - 1);  // fft-shift, nativedsp.cpp:77
-            if (row) row[o] = db;
-            if (ring) ring[o] = db;
+        for (int j = 0; j < CH; j++) {
+            const float2 x = convert_raw<FMT>(raw[j]);
+            v[j0 + j] = make_float2(x.x * w[j], x.y * w[j]);  // NativeDsp.kt:55-58 (fp32 multiply)
         }
+        if (j0 + CH < S) __builtin_amdgcn_sched_barrier(0);
     }
+    dft<S>(v);  // v[s] = sum_j x w W_S^{j s}
+    // m >> 7 is the same for the 64 lanes of a wave (256-thread blocks of consecutive m):
+    // the C factors are scalar loads
+    const int khi = __builtin_amdgcn_readfirstlane(m >> 7), klo = m & 127;
+    constexpr int mc = M >> 7;
+    // W_N^{m s} = C (1 + delta): the small correction C * delta is added last, so the
+    // twiddle carries C's rounding and one add instead of a full product's.  Chunks
+    // of 8 (scheduling barriers) keep the delta loads from all being live at once.
+#pragma unroll
+    for (int s0 = 0; s0 < S; s0 += 8) {
+        float2 d[8];
+#pragma unroll
+        for (int s = s0; s < s0 + 8 && s < S; s++) d[s - s0] = a.tw_d[s * 128 + klo];
+#pragma unroll
+        for (int s = (s0 ? s0 : 1); s < s0 + 8 && s < S; s++) {
+            const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, d[s - s0]);
+            v[s] = cmul(v[s], make_float2(c.x + corr.x, c.y + corr.y));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
+#pragma unroll
+    for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
 }
 
 template <int S>
-static hipError_t launch_s(const DitLaunch &a) {
-    const dim3 grid((1 << a.logm) / 256, a.n_frames);
-    if (a.complex_out) hipLaunchKernelGGL((dit_combine_kernel<S, true>), grid, dim3(256), 0, a.stream, a);
-    else hipLaunchKernelGGL((dit_combine_kernel<S, false>), grid, dim3(256), 0, a.stream, a);
+static hipError_t launch_s(const DifLaunch &a) {
+    const dim3 grid((1 << kDitLogM) / 256, a.n_frames);
+    switch (a.fmt) {
+    case 0: hipLaunchKernelGGL((dif_front_kernel<S, 0>), grid, dim3(256), 0, a.stream, a); break;
+    case 1: hipLaunchKernelGGL((dif_front_kernel<S, 1>), grid, dim3(256), 0, a.stream, a); break;
+    case 2: hipLaunchKernelGGL((dif_front_kernel<S, 2>), grid, dim3(256), 0, a.stream, a); break;
+    case 3: hipLaunchKernelGGL((dif_front_kernel<S, 3>), grid, dim3(256), 0, a.stream, a); break;
+    case 4: hipLaunchKernelGGL((dif_front_kernel<S, 4>), grid, dim3(256), 0, a.stream, a); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
-hipError_t launch_dit_combine(const DitLaunch &a) {
+hipError_t launch_dif_front(const DifLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
-    switch (a.logn - a.logm) {
+    switch (a.logn - kDitLogM) {
     case 3: return launch_s<8>(a);
     case 4: return launch_s<16>(a);
     case 5: return launch_s<32>(a);
@@ -79,7 +107,33 @@ hipError_t launch_dit_combine(const DitLaunch &a) {
     }
 }
 
-void dit_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d) {
+// Caller rows of the large-N pair: kernel B writes dB rows residue-major (block s
+// holds bins S q + s, like the ring); this puts them in natural order,
+// rows[f][q S + s] = cols[f][s][q], through a 64-column LDS tile (coalesced both ways).
+template <int S>
+__global__ void __launch_bounds__(256) cols_to_rows_kernel(const float *cols, float *rows) {
+    constexpr int M = 1 << kDitLogM;
+    __shared__ float tile[S][65];  // odd pitch: the column-order reads are conflict free
+    const int q0 = blockIdx.x * 64;
+    const size_t off = (size_t)blockIdx.y * S * M;
+    for (int e = threadIdx.x; e < S * 64; e += 256) tile[e >> 6][e & 63] = cols[off + (size_t)(e >> 6) * M + q0 + (e & 63)];
+    __syncthreads();
+    for (int e = threadIdx.x; e < S * 64; e += 256) rows[off + (size_t)q0 * S + e] = tile[e % S][e / S];
+}
+
+hipError_t launch_cols_to_rows(const float *cols, float *rows, int n_frames, int logn, hipStream_t st) {
+    if (n_frames <= 0) return hipSuccess;
+    const dim3 grid((1 << kDitLogM) / 64, n_frames);
+    switch (logn - kDitLogM) {
+    case 3: hipLaunchKernelGGL((cols_to_rows_kernel<8>), grid, dim3(256), 0, st, cols, rows); break;
+    case 4: hipLaunchKernelGGL((cols_to_rows_kernel<16>), grid, dim3(256), 0, st, cols, rows); break;
+    case 5: hipLaunchKernelGGL((cols_to_rows_kernel<32>), grid, dim3(256), 0, st, cols, rows); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+void dif_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d) {
     const int m = 1 << kDitLogM, s = 1 << (logn - kDitLogM), mc = m >> 7;
     const double n = (double)(1 << logn);
     auto w = [&](double e) {  // exp(-2 pi i e / N), correctly rounded from double
@@ -90,7 +144,10 @@ void dit_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d) {
     d.assign((size_t)s * 128, make_float2(1.f, 0.f));
     for (int r = 0; r < s; r++) {
         for (int h = 0; h < mc; h++) c[(size_t)r * mc + h] = w(std::fmod((double)r * 128.0 * h, n));
-        for (int l = 0; l < 128; l++) d[(size_t)r * 128 + l] = w((double)r * l);
+        for (int l = 0; l < 128; l++) {  // delta = W_N^{r l} - 1: (-2 sin^2(a/2), sin a) from double
+            const double ang = -2.0 * M_PI * (double)r * l / n, h = std::sin(0.5 * ang);
+            d[(size_t)r * 128 + l] = make_float2((float)(-2.0 * h * h), (float)std::sin(ang));
+        }
     }
 }
 

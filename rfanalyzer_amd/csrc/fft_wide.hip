@@ -408,9 +408,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int tid = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::HALFP;
 
-    // decimation in time: items grouped 8 frames x S residues (see body()), frames padded to 8
-    const bool dit = RS == 1 && COMPLEX_OUT && a.dit_ss > 1;
-    const int work = dit ? ((a.n_frames + 7) / 8) * 8 * a.dit_ss : a.n_frames;
+    // large-N kernel B (FMT == kFmtDif): S column residues per frame, one work item each
+    constexpr bool dif = FMT == kFmtDif;
+    static_assert(!dif || (RS == 1 && G::SLOTS == 1), "large-N kernel B: one 32 K residue per workgroup");
+    const int work = dif ? a.n_frames * a.dif_ss : a.n_frames;
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
@@ -495,17 +496,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         asm volatile("s_mov_b32 %0, 0" : "=s"(z));
         const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
         int frame, r;
-        int dit_r = 0;  // decimation-in-time residue (a.dit_ss > 1): sub-frame = (frame, dit_r)
+        int dif_r = 0;  // large-N kernel B: column residue s of the frame (bins S q + s)
         if constexpr (RS == 1) {
             frame = u * G::SLOTS + slot;
             r = 0;
-            if (dit) {
-                // the S residues (strided sub-frames) of a frame on one XCD (blocks b, b+8,
-                // ... share one), dispatched together: each XCD fetches a frame's lines
-                // once into its L2 and its S workgroups share them (speed only)
-                const int g = u / (8 * a.dit_ss), rem = u - g * (8 * a.dit_ss);
-                dit_r = rem >> 3;
-                frame = g * 8 + (rem & 7);
+            if constexpr (dif) {
+                frame = u / a.dif_ss;
+                dif_r = u - frame * a.dif_ss;
             }
         } else {
             // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
@@ -514,14 +511,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             frame = g * 8 + (rem & 7);
         }
         const bool active = frame < a.n_frames;
-        // sample stride and full frame length (decimation in time: S and S*M)
-        const int ss = (RS == 1 && COMPLEX_OUT && a.dit_ss > 1) ? a.dit_ss : 1;
         constexpr int SB0 = FMT == 4 ? 4 : BPS;
-        // inactive slots read zeros (num_records = 0) and store nothing
+        // inactive slots read zeros (num_records = 0) and store nothing; kernel B's
+        // residue s of a frame is the contiguous z_s block of the scratch
         const rsrc_t in_rs =
-            make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride + (size_t)dit_r * SB0,
-                      active ? (unsigned)(n * ss * BPS - dit_r * SB0) : 0u);
-        const int planar_im = n * ss * 4;
+            make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride + (size_t)dif_r * (M * 8),
+                      active ? (unsigned)(n * BPS) : 0u);
+        const int planar_im = n * 4;
 
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
@@ -540,8 +536,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (RS == 1) {
             // all PT raw samples of the thread in flight at once (buffer loads need
             // no address registers), then the window (L2-resident) and convert.
-            const rsrc_t w_rs = make_rsrc(a.window + (size_t)dit_r * n, n * 4);
-            const int SB = SB0 * ss;  // bytes between consecutive samples of this (sub-)frame
+            const rsrc_t w_rs = make_rsrc(a.window, dif ? 0 : n * 4);
+            constexpr int SB = SB0;  // bytes between consecutive samples
             typename Raw<FMT>::T raw[PT];
     #pragma unroll
             for (int idx = 0; idx < PT; idx++) {
@@ -553,7 +549,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     #pragma unroll
             for (int idx = 0; idx < PT; idx++) {
                 const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
-                const float w = (DIAG & 16) ? 1.0f : buf_load_f32(w_rs, tid * 4, so * 4);
+                // kernel B's input is already windowed (kernel A)
+                const float w = ((DIAG & 16) || dif) ? 1.0f : buf_load_f32(w_rs, tid * 4, so * 4);
                 const float2 x = convert_raw<FMT>(raw[idx]);
                 v[idx] = make_float2(x.x * w, x.y * w);  // NativeDsp.kt:55-58 (fp32 multiply)
             }
@@ -603,16 +600,21 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             return;
         }
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
+        // (kernel B of the large-N pair: kk = s + S*(...) with the runtime S = dif_ss and
+        // s = dif_r; the stride and frame length below are then uniform runtime values)
+        const int ors = dif ? a.dif_ss : RS, orr = dif ? dif_r : r;
+        const int on = dif ? M * a.dif_ss : n;
         if constexpr (COMPLEX_OUT) {
-            const rsrc_t o_rs = make_rsrc(a.complex_out + ((size_t)frame * ss + dit_r) * n, n * 8);
+            const rsrc_t o_rs = make_rsrc(a.complex_out + (size_t)frame * on, on * 8);
     #pragma unroll
             for (int b = 0; b < PT / G::R2; b++)
     #pragma unroll
                 for (int t = 0; t < G::R2; t++)
-                    buf_store_f32x2(v[b * G::R2 + t], o_rs, (RS * tid + r) * 8,
-                                    RS * (G::TPF * b + t * (M / G::R2)) * 8);
+                    buf_store_f32x2(v[b * G::R2 + t], o_rs, (ors * tid + orr) * 8,
+                                    ors * (G::TPF * b + t * (M / G::R2)) * 8);
         } else {
-            constexpr float db_off = -kDbPerLog2 * (float)(2 * (LOGM + (RS == 1 ? 0 : RS == 2 ? 1 : RS == 4 ? 2 : 3)));
+            constexpr float db_off_c = -kDbPerLog2 * (float)(2 * (LOGM + (RS == 1 ? 0 : RS == 2 ? 1 : RS == 4 ? 2 : 3)));
+            const float db_off = dif ? db_offset(LOGM + (31 - __builtin_clz(a.dif_ss))) : db_off_c;
             const bool to_ring = a.ring && frame >= a.ring_first;
             int rr = 0;
             if (to_ring) {
@@ -622,11 +624,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // ring in residue-major order (ring_pos, fft_kernels.h) when the engine asks for
             // it: residue r's M bins are one contiguous block, so this workgroup's stores
             // cover whole lines; caller rows are always natural (fft-shifted) order
-            const bool rm = RS > 1 && a.ring_logrs > 0;
-            const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n : nullptr, a.rows ? n * 4 : 0);
-            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * n + (rm ? (size_t)r * M : 0) : nullptr,
-                                             to_ring ? (rm ? M : n) * 4 : 0);
-            const int vo = (RS * tid + r) * 4;
+            const bool rm = (RS > 1 || dif) && a.ring_logrs > 0;
+            // kernel B (dif): rows residue-major too, block s (the engine reorders them)
+            const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * on + (dif ? (size_t)orr * M : 0) : nullptr,
+                                            a.rows ? (dif ? M : on) * 4 : 0);
+            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * on + (rm ? (size_t)orr * M : 0) : nullptr,
+                                             to_ring ? (rm ? M : on) * 4 : 0);
+            const int vo = (ors * tid + orr) * 4;
             // one uniform branch per item, not per store
             auto epilogue = [&](auto nat_c, auto ring_c, auto rm_c) {
     #pragma unroll
@@ -636,13 +640,16 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                         const float2 x = v[b * G::R2 + t];
                         const float db = db_unscaled(x, db_off);  // nativedsp.cpp:73-78
                         // fft-shift (nativedsp.cpp:77): out[(kk + N/2) mod N]; the lane part never wraps
-                        const int so = ((RS * (G::TPF * b + t * (M / G::R2)) + n / 2) & (n - 1)) * 4;
+                        const int so = ((ors * (G::TPF * b + t * (M / G::R2)) + on / 2) & (on - 1)) * 4;
                         // residue-major: sub-bin i = tid + TPF b + t M/R2 at (i + M/2) mod M of the block
                         const int so_rm = ((G::TPF * b + t * (M / G::R2) + M / 2) & (M - 1)) * 4;
                         if constexpr (DIAG & 2) {
                             asm volatile("" ::"v"(db));
                         } else {
-                            if constexpr (decltype(nat_c)::value) buf_store_f32(db, row_rs, vo, so);
+                            if constexpr (decltype(nat_c)::value) {
+                                if constexpr (dif) buf_store_f32(db, row_rs, tid * 4, so_rm);
+                                else buf_store_f32(db, row_rs, vo, so);
+                            }
                             if constexpr (decltype(ring_c)::value) {
                                 if constexpr (decltype(rm_c)::value) buf_store_f32(db, ring_rs, tid * 4, so_rm);
                                 else buf_store_f32(db, ring_rs, vo, so);
@@ -655,7 +662,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             using F_ = std::false_type;
             pending_st = (a.rows ? PT : 0) + (to_ring ? PT : 0);
             if (a.rows && to_ring) {
-                if constexpr (RS > 1) {
+                if constexpr (RS > 1 || dif) {
                     if (rm) epilogue(T_{}, T_{}, T_{});
                     else epilogue(T_{}, T_{}, F_{});
                 } else {
@@ -664,7 +671,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             } else if (a.rows) {
                 epilogue(T_{}, F_{}, F_{});
             } else if (to_ring) {
-                if constexpr (RS > 1) {
+                if constexpr (RS > 1 || dif) {
                     if (rm) epilogue(F_{}, T_{}, T_{});
                     else epilogue(F_{}, T_{}, F_{});
                 } else {
@@ -704,7 +711,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
         if (e != hipSuccess) return e;
         attr = true;
     }
-    const int work = (RS == 1 && CO && a.dit_ss > 1) ? ((a.n_frames + 7) / 8) * 8 * a.dit_ss : a.n_frames;
+    const int work = FMT == kFmtDif ? a.n_frames * a.dif_ss : a.n_frames;
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;
@@ -996,6 +1003,7 @@ static hipError_t launch_w64(const FftLaunch &a) {
 }
 
 int ring_logrs_for(int logn, int wide_big, int w64) {
+    if (logn > 17 && logn <= kMaxLogN) return logn - kDitLogM;  // large-N kernel B: block s of bins S q + s
     if (!wide_supported(logn) || logn <= 14) return 0;
     if (logn == 16 && wide_big == 15 && w64) return 6;
     return logn - wide_logm(logn, wide_big);
@@ -1004,16 +1012,6 @@ int ring_logrs_for(int logn, int wide_big, int w64) {
 template <int LOGM, int PT, int RS, bool CO>
 static hipError_t wide_by_fmt(const FftLaunch &a) {
     if constexpr (CO) {
-        if constexpr (LOGM == kDitLogM && RS == 1) {  // kernel A of the large-N path: every format
-            switch (a.fmt) {
-            case 0: return launch_wide_one<LOGM, PT, RS, 0, true>(a);
-            case 1: return launch_wide_one<LOGM, PT, RS, 1, true>(a);
-            case 2: return launch_wide_one<LOGM, PT, RS, 2, true>(a);
-            case 3: return launch_wide_one<LOGM, PT, RS, 3, true>(a);
-            case 4: return launch_wide_one<LOGM, PT, RS, 4, true>(a);
-            default: return hipErrorInvalidValue;
-            }
-        }
         return a.fmt == 3 ? launch_wide_one<LOGM, PT, RS, 3, true>(a) : hipErrorInvalidValue;
     } else {
         using G = WGeo<LOGM, PT>;
@@ -1098,9 +1096,9 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         default: return hipErrorInvalidValue;
         }
     }
-    if (a.dit_ss > 1) {  // kernel A of the large-N decimation-in-time path
-        if (!co) return hipErrorInvalidValue;
-        return wide_by_fmt<kDitLogM, 32, 1, true>(a);
+    if (a.fmt == kFmtDif) {  // kernel B of the large-N pair (dB rows / ring, or the ordered spectrum)
+        if (a.dif_ss < 8 || a.dif_ss > 32) return hipErrorInvalidValue;
+        return co ? launch_wide_one<kDitLogM, 32, 1, kFmtDif, true>(a) : launch_wide_one<kDitLogM, 32, 1, kFmtDif, false>(a);
     }
     if (a.logn >= 15 && a.wide_big == 15) {
         switch (a.logn) {

@@ -71,17 +71,18 @@ def test_ring_indices_and_rows_match_processor_restatement(rfa):
     e.close()
 
 
-@pytest.mark.parametrize("n", [256, 65536, 131072])
+@pytest.mark.parametrize("n", [256, 65536, 131072, 1048576])
 @pytest.mark.parametrize("new_freq,new_sr", [(100 + 37, 1000), (100 - 300, 1000), (100 + 999, 1000), (100, 2000)])
 def test_retune_shift_and_clear(rfa, n, new_freq, new_sr):
     """FftProcessor.kt:197-220 shift / clear; at 64 K and 128 K the device ring is stored
-    residue-major (rfa_get_ring_order 2 / 4) and the shift runs in that order."""
+    residue-major (rfa_get_ring_order 2 / 4), at 1 M in the large-N kernel B's column
+    order (32 blocks of bins 32 q + s), and the shift runs in that order."""
     rows_r = 4
     data = np.random.default_rng(4).integers(-128, 128, size=2 * n * 3, dtype=np.int8).tobytes()
     ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, 3, None, oracle.WIN_BLACKMAN)
     p = processor.FftProcessorRef(n, rows_r, peak_hold=True)
     e = rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=rows_r)
-    assert e.ring_order == {65536: 2, 131072: 4}.get(n, 1)
+    assert e.ring_order == {65536: 2, 131072: 4, 1048576: 32}.get(n, 1)
     e.set_tuning(100, 1000)
     e.process(data[: 2 * 2 * n], 2, rows=False)
     p.push(ref_rows[0], 100, 1000)
