@@ -70,6 +70,7 @@ def parse(argv=None):
     p.add_argument("--pool-mib", type=int, default=768, help="input pool size (> Infinity Cache)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget (0 = skip)")
     p.add_argument("--f32-steps", type=int, default=4, help="steps of the float32-input companion run (0 = skip)")
+    p.add_argument("--c5-steps", type=int, default=3, help="steps of the 1 M-point (config 5) companion (0 = skip)")
     p.add_argument("--demod-steps", type=int, default=5,
                    help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
     p.add_argument("--profile-every", type=int, default=8,
@@ -599,6 +600,24 @@ def main():
                          "roofline_achieved_GBps": round(alg32 / (k32 * 1e-3) / 1e9, 1),
                          "roofline_frac": round(alg32 / (k32 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                          "alg_bytes_per_launch": alg32}
+    if single and args.mode == "streams" and n != (1 << 20) and args.c5_steps > 0:
+        # config 5's per-GPU stream: 1 M-point FFT, same stateful settings, reported beside
+        # the headline (never `value`); its main-kernel time spans the large-N pair
+        import copy
+        a5 = copy.copy(args)
+        a5.fft_size, a5.frames, a5.calls_per_step = 1 << 20, 16, 30
+        el5, _, k5, name5 = run_streams(a5, ranks, fmt, args.c5_steps, 1, 203)
+        alg5 = a5.frames * a5.fft_size * (s_in + 4)
+        result["config5"] = {"workload": f"config5 per GPU: 1048576-pt FFT, {args.window}, {fmt} IQ, "
+                                         f"{'EMA' if args.avg == 'ema' else args.avg} + peak-hold, ring "
+                                         f"{args.ring_rows} rows, 16 frames per call",
+                             "value": round(args.c5_steps * a5.calls_per_step * a5.frames * a5.fft_size / el5 / 1e6, 2),
+                             "unit": "Msamples/s", "ms_per_step": round(el5 * 1e3 / args.c5_steps, 4),
+                             "kernel_ms": round(k5, 4), "kernel": name5,
+                             "roofline_achieved_GBps": round(alg5 / (k5 * 1e-3) / 1e9, 1),
+                             "roofline_frac": round(alg5 / (k5 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                             "alg_bytes_per_launch": alg5,
+                             "note": "kernel_ms = the whole large-N launch (front kernel + 32 K kernel B)"}
     if single and args.demod_steps > 0:
         result["demod"] = demod_companion(torch, ranks.device, args.demod_steps)
     if ranks.rank == 0 and ranks.world == 1 and args.cpu_seconds > 0 and args.mode == "streams":

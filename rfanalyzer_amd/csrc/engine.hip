@@ -460,7 +460,9 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
             if (hipMemcpy(*u.dst, u.src, u.bytes, hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
         }
         // scratch per kernel pair <= 128 MB so it stays in the 256 MB Infinity Cache
-        h->dit_frames = (int)std::max<size_t>(1, ((size_t)128 << 20) / ((size_t)n * sizeof(float2)));
+        size_t mb = 128;
+        if (const char *d = std::getenv("RFA_DIT_SCRATCH_MB")) mb = (size_t)std::max(8, std::atoi(d));  // A/B only
+        h->dit_frames = (int)std::max<size_t>(1, (mb << 20) / ((size_t)n * sizeof(float2)));
     }
     if (rfa::wide_supported(logn)) {
         std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn, h->wide_big));
