@@ -232,7 +232,9 @@ RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, flo
  * ring row lives at element (t mod RS) * (N/RS) + t / RS.  RS = 1 is natural
  * order; the N = 64 K / 128 K kernels compute a frame as RS residue sub-FFTs and
  * store each residue's bins as one contiguous block (whole cache lines per
- * workgroup).  Every rfa_* consumer of the ring handles this internally. */
+ * workgroup); N = 256 K .. 1 M use RS = N / 32768 (the large-N kernel B writes
+ * the bins S q + s of column s as block s).  Every rfa_* consumer of the ring
+ * handles this internally. */
 RFA_API int rfa_get_ring_order(const rfa_handle *h, int32_t *residues);
 
 /* Reference-seam entry points (host arrays, synchronous).  They use the

@@ -1168,6 +1168,8 @@ int rfa_set_profiling(rfa_handle *h, int enable) {
 
 const char *rfa_main_kernel_name(const rfa_handle *h) {
     if (!h) return "";
+    if (h->logn > 17) return "dif_front_kernel+fft_wide_kernel";  // the large-N pair (fft_large.hip)
+    if (h->w64 && h->logn == 16) return "fft_w64_kernel";
     const bool wide = h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(h->logn);
     return wide ? "fft_wide_kernel" : "fft_rows_kernel";
 }

@@ -30,47 +30,68 @@
 
 namespace rfa {
 
+#ifndef RFA_DIF_ABL
+#define RFA_DIF_ABL 0  // ablations (A/B builds only): 1 no z stores, 2 no twiddles
+#endif
 template <int S, int FMT>
 __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     constexpr int M = 1 << kDitLogM, n = S * M;
     constexpr int SB = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 || FMT == 4) ? 4 : 8;  // bytes per sample (per plane)
     constexpr int PLANES = FMT == 4 ? 2 : 1;
-    // the block's raw tile: S rows x 256 consecutive samples (per plane), fetched with
-    // 16-B loads all in flight at once, then read per thread from LDS
-    constexpr int ROWB = 256 * SB, PPR = ROWB / 16, NP = S * PPR * PLANES;
+    // 8/16-bit formats: the block's raw tile (S rows x 256 consecutive samples) is
+    // fetched with 16-B loads all in flight at once, then read per thread from LDS.
+    // f32 formats load straight into registers (8 B per lane is already a wide
+    // access; their 64 KB tile would halve the resident blocks: measured slower).
+    constexpr bool TILE = FMT <= 2;
+    constexpr int ROWB = 256 * SB, PPR = ROWB / 16, NP = TILE ? S * PPR : 256;
     static_assert(NP % 256 == 0, "whole 16-B pieces per thread");
     __shared__ uint4 tile[NP];
     const int m0 = blockIdx.x * 256, m = m0 + threadIdx.x;
     const int f = blockIdx.y;
     const rsrc_t in_rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * SB * PLANES);
     const rsrc_t w_rs = make_rsrc(a.window, n * 4);
-    {
-        uint4 q[NP / 256];
-#pragma unroll
-        for (int i = 0; i < NP / 256; i++) {
-            const int e = i * 256 + threadIdx.x;
-            const int pl = e / (S * PPR), j = (e / PPR) % S, pc = e % PPR;
-            q[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                 in_rs, pc * 16, pl * n * 4 + (j * M + m0) * SB, 0));
-        }
-#pragma unroll
-        for (int i = 0; i < NP / 256; i++) tile[i * 256 + threadIdx.x] = q[i];
-    }
-    float w[S];
-#pragma unroll
-    for (int j = 0; j < S; j++) w[j] = buf_load_f32(w_rs, m * 4, j * M * 4);
-    __syncthreads();
-    const uint8_t *tb = reinterpret_cast<const uint8_t *>(tile);
     float2 v[S];
+    if constexpr (TILE) {
+        {
+            uint4 q[NP / 256];
 #pragma unroll
-    for (int j = 0; j < S; j++) {
-        typename Raw<FMT>::T raw;
-        if constexpr (FMT == 4)
-            raw = make_float2(*reinterpret_cast<const float *>(tb + j * ROWB + threadIdx.x * 4),
-                              *reinterpret_cast<const float *>(tb + S * ROWB + j * ROWB + threadIdx.x * 4));
-        else raw = *reinterpret_cast<const typename Raw<FMT>::T *>(tb + j * ROWB + threadIdx.x * SB);
-        const float2 x = convert_raw<FMT>(raw);
-        v[j] = make_float2(x.x * w[j], x.y * w[j]);  // NativeDsp.kt:55-58 (fp32 multiply)
+            for (int i = 0; i < NP / 256; i++) {
+                const int e = i * 256 + threadIdx.x;
+                const int j = e / PPR, pc = e % PPR;
+                q[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(in_rs, pc * 16, (j * M + m0) * SB, 0));
+            }
+#pragma unroll
+            for (int i = 0; i < NP / 256; i++) tile[i * 256 + threadIdx.x] = q[i];
+        }
+        float w[S];
+#pragma unroll
+        for (int j = 0; j < S; j++) w[j] = buf_load_f32(w_rs, m * 4, j * M * 4);
+        __syncthreads();
+        const uint8_t *tb = reinterpret_cast<const uint8_t *>(tile);
+#pragma unroll
+        for (int j = 0; j < S; j++) {
+            const float2 x = convert_raw<FMT>(*reinterpret_cast<const typename Raw<FMT>::T *>(tb + j * ROWB + threadIdx.x * SB));
+            v[j] = make_float2(x.x * w[j], x.y * w[j]);  // NativeDsp.kt:55-58 (fp32 multiply)
+        }
+    } else {
+        // chunks of 8 rows (scheduling barriers): fewer live registers, more waves per SIMD
+        constexpr int CH = S < 8 ? S : 8;
+#pragma unroll
+        for (int j0 = 0; j0 < S; j0 += CH) {
+            typename Raw<FMT>::T raw[CH];
+            float w[CH];
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                raw[j] = buf_load_raw<FMT>(in_rs, m * SB, (j0 + j) * M * SB, n * 4);
+                w[j] = buf_load_f32(w_rs, m * 4, (j0 + j) * M * 4);
+            }
+#pragma unroll
+            for (int j = 0; j < CH; j++) {
+                const float2 x = convert_raw<FMT>(raw[j]);
+                v[j0 + j] = make_float2(x.x * w[j], x.y * w[j]);  // NativeDsp.kt:55-58 (fp32 multiply)
+            }
+            if (j0 + CH < S) __builtin_amdgcn_sched_barrier(0);
+        }
     }
     dft<S>(v);  // v[s] = sum_j x w W_S^{j s}
     // m >> 7 is the same for the 64 lanes of a wave (256-thread blocks of consecutive m):
@@ -81,7 +102,7 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     // twiddle carries C's rounding and one add instead of a full product's.  Chunks
     // of 8 (scheduling barriers) keep the delta loads from all being live at once.
 #pragma unroll
-    for (int s0 = 0; s0 < S; s0 += 8) {
+    for (int s0 = 0; s0 < S && !(RFA_DIF_ABL & 2); s0 += 8) {
         float2 d[8];
 #pragma unroll
         for (int s = s0; s < s0 + 8 && s < S; s++) d[s - s0] = a.tw_d[s * 128 + klo];
@@ -94,7 +115,10 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     }
     const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
 #pragma unroll
-    for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
+    for (int s = 0; s < S; s++) {
+        if constexpr (RFA_DIF_ABL & 1) asm volatile("" ::"v"(v[s].x), "v"(v[s].y));
+        else buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
+    }
 }
 
 template <int S>
