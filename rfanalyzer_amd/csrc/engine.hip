@@ -41,6 +41,7 @@ struct rfa_handle {
     float *d_dit_db = nullptr;        // caller rows of a batch, residue-major, before cols_to_rows
     size_t d_dit_db_cap = 0;
     int dit_frames = 1;               // frames per kernel-A/B pair (scratch <= kDitScratch)
+    int dif_pipe = 6;                 // RFA_DIF_PIPE: frame groups of the pipelined front kernel (8-bit input; 0 off)
     int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
     int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
     long long stagger_ns = 0;         // RFA_STAGGER_NS
@@ -235,6 +236,7 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         A.tw_c = h->d_dit_c;
         A.tw_d = h->d_dit_d;
         A.z = h->d_dit_y;
+        A.pipe = h->dif_pipe;
         A.stream = a.stream;
         hipError_t e = rfa::launch_dif_front(A);
         if (e != hipSuccess) return e;
@@ -473,6 +475,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_KERNEL")) h->variant = std::string(d) == "narrow" ? 1 : 0;
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
     if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
+    if (const char *d = std::getenv("RFA_DIF_PIPE")) h->dif_pipe = std::max(0, std::atoi(d));
     if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
     {

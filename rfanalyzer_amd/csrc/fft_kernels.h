@@ -103,6 +103,7 @@ struct DifLaunch {
     const float2 *tw_c = nullptr;   // [S][M/128]  W_N^{s * 128 * mhi}
     const float2 *tw_d = nullptr;   // [S][128]    W_N^{s * mlo} - 1
     float2 *z = nullptr;            // scratch [n_frames][S][M]
+    int pipe = 6;                   // 8-bit, 16-B aligned frames: pipelined kernel with `pipe` frame groups (0: off)
     hipStream_t stream = nullptr;
 };
 constexpr int kDitLogM = 15;

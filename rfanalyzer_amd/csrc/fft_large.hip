@@ -22,7 +22,9 @@
 // the scratch stays in the 256 MB Infinity Cache.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdint>
 #include <vector>
 
 #include "fft_common.h"
@@ -121,9 +123,87 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     }
 }
 
+// 8-bit formats, persistent and pipelined: block b owns the 256 columns
+// (b % 128) * 256 .. + 255 and frames b / 128, + G, + 2G, ... (G = frame groups).
+// The window values of its columns stay in registers and the D table in LDS
+// across its frames; the next frame's tile is fetched by LDS-DMA (16 B per lane,
+// no VGPRs) right after every wave has read the current one, so it lands while
+// this frame is transformed and its z stores drain: loads and stores of a block
+// overlap instead of every block loading, then storing, in lock step.
+template <int S, int FMT>
+__global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int groups) {
+    static_assert(FMT <= 1, "8-bit formats");
+    constexpr int M = 1 << kDitLogM, n = S * M, mc = M >> 7;
+    constexpr int SB = 2;
+    constexpr int ROWB = 256 * SB, TILEB = S * ROWB, NPIECE = TILEB / 1024, PPW = NPIECE / 4;
+    constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;  // tile rows per 1 KiB piece, lanes per row
+    static_assert(NPIECE % 4 == 0 && RPP >= 1, "whole pieces per wave");
+    __shared__ __attribute__((aligned(16))) uint8_t tile[TILEB];
+    __shared__ float2 dtab[S * 128];
+    const int bx = blockIdx.x % (M / 256), g0 = blockIdx.x / (M / 256);
+    const int m0 = bx * 256, m = m0 + threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const unsigned tbase = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)tile;
+    auto stage = [&](int f) {  // this wave's PPW pieces of frame f's tile (inline asm: see stage_frame)
+        const rsrc_t rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * SB);
+#pragma unroll
+        for (int i = 0; i < PPW; i++) {
+            const int pc = wave * PPW + i, j = pc * RPP + lane / LPR;
+            const int voff = (j * M + m0) * SB + (lane % LPR) * 16;
+            unsigned keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                "buffer_load_dwordx4 %2, %3, 0 offen lds\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "s"(tbase + pc * 1024), "v"(voff), "s"(rs)
+                : "memory");
+        }
+    };
+    for (int e = threadIdx.x; e < S * 128; e += 256) dtab[e] = a.tw_d[e];
+    const rsrc_t w_rs = make_rsrc(a.window, n * 4);
+    float w[S];
+#pragma unroll
+    for (int j = 0; j < S; j++) w[j] = buf_load_f32(w_rs, m * 4, j * M * 4);
+    const int khi = __builtin_amdgcn_readfirstlane(m >> 7), klo = m & 127;
+    if (g0 < a.n_frames) stage(g0);
+    bool first = true;
+    for (int f = g0; f < a.n_frames; f += groups) {
+        // this frame's tile has landed (younger than its DMA: the previous frame's S stores)
+        if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(S) : "memory");
+        first = false;
+        float2 v[S];
+#pragma unroll
+        for (int j = 0; j < S; j++) {
+            const auto raw = *reinterpret_cast<const typename Raw<FMT>::T *>(tile + j * ROWB + threadIdx.x * SB);
+            const float2 x = convert_raw<FMT>(raw);
+            v[j] = make_float2(x.x * w[j], x.y * w[j]);  // NativeDsp.kt:55-58 (fp32 multiply)
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave has read the tile
+        if (f + groups < a.n_frames) stage(f + groups);
+        dft<S>(v);
+#pragma unroll
+        for (int s = 1; s < S; s++) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel
+            const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, dtab[s * 128 + klo]);
+            v[s] = cmul(v[s], make_float2(c.x + corr.x, c.y + corr.y));
+        }
+        const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
+#pragma unroll
+        for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
+    }
+}
+
 template <int S>
 static hipError_t launch_s(const DifLaunch &a) {
     const dim3 grid((1 << kDitLogM) / 256, a.n_frames);
+    // pipelined kernel: 8-bit input (16-bit measured slower: its 64 KB of LDS halves the resident blocks)
+    if (a.pipe > 0 && a.fmt <= 1 && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0) {
+        const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = 128 x groups
+        const dim3 pg((1 << kDitLogM) / 256 * groups);
+        if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(256), 0, a.stream, a, groups);
+        else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(256), 0, a.stream, a, groups);
+        return hipGetLastError();
+    }
     switch (a.fmt) {
     case 0: hipLaunchKernelGGL((dif_front_kernel<S, 0>), grid, dim3(256), 0, a.stream, a); break;
     case 1: hipLaunchKernelGGL((dif_front_kernel<S, 1>), grid, dim3(256), 0, a.stream, a); break;
