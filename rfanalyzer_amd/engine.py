@@ -103,7 +103,9 @@ class SpectrumEngine:
     def process_tensor(self, t, n_frames: int | None = None, frame_stride: int = 0, rows=None) -> None:
         """torch.cuda tensors (uint8/int8/float32 input, float32 rows).  Enqueued on torch's
         current stream: ordered after the op that produced ``t`` and before later torch ops
-        that read ``rows``."""
+        that read ``rows``.  Import torch before this package when mixing the two: torch's
+        wheel bundles its own libamdhip64.so; loaded first, librfa binds to that same
+        runtime, loaded second it finds the system one already mapped and torch sees no GPU."""
         import torch
 
         cur = torch.cuda.current_stream(t.device).cuda_stream

@@ -2,7 +2,8 @@
 float64 oracle.  Tolerance: 0.01 dB (north star), identical argmax bins."""
 import numpy as np
 import pytest
-
+import torch  # noqa: F401  -- before librfa: torch's bundled HIP runtime (libamdhip64.so, ROCm 7.0) must
+#                                 load first; librfa then resolves to it (same soname), one runtime per process
 import golden_util as gu
 import oracle
 import signals
@@ -166,3 +167,29 @@ def test_large_n_seams(rfa, n):
         dsp.performFFTAndLogMag(x, out)
         assert gu.pffft_diff(out, oracle.ref_fft_logmag(x)) <= gu.DB_TOL
     dsp.close()
+
+
+@pytest.mark.parametrize("fmt", ["s8", "u8"])
+def test_large_n_front_kernel_alignment_paths(rfa, fmt):
+    """N = 1 M, 8-bit input: 16-byte aligned frames take the pipelined persistent front
+    kernel (LDS-DMA tiles), a misaligned device pointer the one-block-per-tile kernel.
+    Both do the same fp32 operations in the same order, so the rows are bit-identical,
+    and both match the oracle; 7 frames over 6 frame groups exercises the uneven split."""
+    import torch  # imported at collection time too (module top): see there
+
+    n, frames = 1 << 20, 7
+    data = signals.frames_bytes(n, frames, fmt, seed=77, tones=((0.0123, 0.3), (-0.41, 0.02)), noise=0.04)
+    raw = np.frombuffer(data, np.uint8)
+    ref = oracle.spectrum_rows(data, signals.FORMATS[fmt], n, frames, None, oracle.WIN_BLACKMAN)
+    out = []
+    with _engine(rfa, n, fmt, "blackman", ring_rows=0) as e:
+        for off in (0, 2):
+            buf = torch.zeros(raw.size + 64, dtype=torch.uint8, device="cuda")
+            buf[off:off + raw.size] = torch.from_numpy(raw.copy()).cuda()
+            rows = torch.empty((frames, n), dtype=torch.float32, device="cuda")
+            e.process_tensor(buf[off:off + raw.size], frames, 0, rows)
+            torch.cuda.synchronize()
+            out.append(rows.cpu().numpy())
+    np.testing.assert_array_equal(out[0], out[1])
+    assert gu.db_diff(out[0], ref) <= gu.DB_TOL
+    gu.assert_same_peak_bins(out[0], np.argmax(ref, 1))
