@@ -47,9 +47,10 @@ def test_window_stats_vs_kotlin(eng):
     assert _close(av, eav)
 
 
-@pytest.mark.parametrize("n", [65536, 131072])
+@pytest.mark.parametrize("n", [65536, 131072, 1048576])
 def test_window_stats_on_residue_major_ring(rfa, n):
-    """The 64 K / 128 K ring is stored residue-major; the window kernel reads bins through ring_pos."""
+    """The 64 K / 128 K ring is stored residue-major, the 1 M ring in the large-N kernel B's
+    column order; the window kernel reads bins through ring_pos."""
     with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=3) as e:
         e.set_tuning(F0, SR)
         e.process(signals.frames_bytes(n, 4, "s8", seed=35, tones=((0.21, 0.3), (-0.2, 0.002)), noise=0.01), 4,

@@ -101,7 +101,7 @@ def test_retune_shift_and_clear(rfa, n, new_freq, new_sr):
     e.close()
 
 
-@pytest.mark.parametrize("n", [65536, 131072])
+@pytest.mark.parametrize("n", [65536, 131072, 1048576])
 def test_boxcar_over_residue_major_ring(rfa, n):
     """rfa_get_boxcar (AnalyzerSurface.kt:710-714 at bin level) gathers the bins of the
     residue-major ring rows back into natural order."""
@@ -154,6 +154,7 @@ def test_chunked_state_with_silent_frames(rfa, batches):
 
 @pytest.mark.parametrize("n,freq,sr,chan", [(4096, 100_000_000, 2_000_000, (100_010_000, 100_060_000)),
                                             (65536, 433_920_000, 20_000_000, (433_000_000, 434_500_000)),
+                                            (1048576, 433_920_000, 250_000_000, (400_000_000, 401_000_000)),
                                             (1024, 100_000_000, 2_000_000, (98_000_000, 99_500_000)),  # below: empty
                                             (1024, 100_000_000, 2_000_000, (99_100_000, 103_000_000))])  # clamped
 def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
@@ -265,24 +266,26 @@ def test_ring_resize_keeps_history(rfa, sizes):
         assert gu.db_diff(e.peaks(), p.peaks) <= gu.DB_TOL
 
 
-def test_fft_size_change_restarts_ring_and_peaks(rfa):
-    """FftProcessor.kt:178-183 (new size -> fresh -9999 ring, writeIndex 0) and :233-236 (peaks re-initialised)."""
-    data = np.random.default_rng(9).integers(-128, 128, size=2 * 2048 * 8, dtype=np.int8).tobytes()
-    rows_a = oracle.spectrum_rows(data, oracle.IN_S8, 1024, 3, None, oracle.WIN_BLACKMAN)
-    rows_b = oracle.spectrum_rows(data[3 * 2 * 1024:], oracle.IN_S8, 2048, 2, None, oracle.WIN_BLACKMAN)
-    p = processor.FftProcessorRef(1024, 4, peak_hold=True, ema_alpha=0.25)
-    with rfa.SpectrumEngine(1024, "blackman", "s8", avg="ema", ema_alpha=0.25, peak_hold=True, ring_rows=4) as e:
+@pytest.mark.parametrize("na,nb", [(1024, 2048), (65536, 1048576), (1048576, 4096)])
+def test_fft_size_change_restarts_ring_and_peaks(rfa, na, nb):
+    """FftProcessor.kt:178-183 (new size -> fresh -9999 ring, writeIndex 0) and :233-236
+    (peaks re-initialised), also across the large-N pair (its scratch, tables and ring order)."""
+    data = np.random.default_rng(9).integers(-128, 128, size=2 * (3 * na + 2 * nb), dtype=np.int8).tobytes()
+    rows_a = oracle.spectrum_rows(data, oracle.IN_S8, na, 3, None, oracle.WIN_BLACKMAN)
+    rows_b = oracle.spectrum_rows(data[3 * 2 * na:], oracle.IN_S8, nb, 2, None, oracle.WIN_BLACKMAN)
+    p = processor.FftProcessorRef(na, 4, peak_hold=True, ema_alpha=0.25)
+    with rfa.SpectrumEngine(na, "blackman", "s8", avg="ema", ema_alpha=0.25, peak_hold=True, ring_rows=4) as e:
         e.set_tuning(100_000_000, 2_000_000)
-        e.process(data[: 3 * 2 * 1024], 3, rows=False)
+        e.process(data[: 3 * 2 * na], 3, rows=False)
         for r in rows_a:
             p.push(r, 100_000_000, 2_000_000)
-        e.set_fft_size(2048)
-        assert e.n == 2048
-        e.process(data[3 * 2 * 1024:3 * 2 * 1024 + 2 * 2 * 2048], 2, rows=False)
+        e.set_fft_size(nb)
+        assert e.n == nb
+        e.process(data[3 * 2 * na:3 * 2 * na + 2 * 2 * nb], 2, rows=False)
         for r in rows_b:
             p.push(r, 100_000_000, 2_000_000)
         ring, ri, wi = e.ring()
-        assert ring.shape == (4, 2048) and (ri, wi) == (p.read_index, p.write_index)
+        assert ring.shape == (4, nb) and (ri, wi) == (p.read_index, p.write_index)
         for row_g, row_p in zip(ring, p.ring):
             if np.all(row_p == -9999):
                 assert np.all(row_g == -9999)
