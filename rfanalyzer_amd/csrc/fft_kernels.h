@@ -38,10 +38,10 @@ struct FftLaunch {
     int fmt = 0;   // rfa_input_format
     int logn = 0;  // N = 1 << logn
     const float *window = nullptr;  // N floats (device); all ones for RFA_WINDOW_NONE
-    const float *window_il = nullptr;
+    const float *window_il = nullptr;  // N > M: window[m + j*M] at [m*RS + j] (wide kernel pre-stage)
     // wide kernel twiddle blob (exact, from double): pass-1 [32][R1] | pass-2 A,B [16][16] |
     // pre-stage pre_a [RS][512] | pre_b [RS][32]   (DESIGN.md "Twiddles")
-    const float2 *wide_tw = nullptr;  // N > 16384: window[m + j*M] at [m*RS + j] (wide kernel pre-stage)
+    const float2 *wide_tw = nullptr;  // wide_twiddles() blob (layout in fft_wide.hip WGeo)
     // twiddle table W_N^s = coarse[s >> tw_shift] * fine[s & ((1<<tw_shift)-1)]
     const float2 *tw_coarse = nullptr;
     const float2 *tw_fine = nullptr;
@@ -77,7 +77,8 @@ struct FftLaunch {
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
 hipError_t launch_fft(const FftLaunch &a);
-// The wide (64 points/thread, 2 workgroups/CU) kernel for N = 2^13..2^17.
+// The wide kernel (32 points per thread, one M-point sub-FFT per workgroup,
+// M = 8 K / 16 K / 32 K) for N = 2^13..2^17, and kernel B of the large-N pair.
 bool wide_supported(int logn);
 // ring order (ring_pos logrs) the main kernel writes for N = 2^logn
 int ring_logrs_for(int logn, int wide_big, int w64);

@@ -17,7 +17,7 @@ import signals
 
 pytestmark = pytest.mark.gpu
 
-N, FRAMES, ALPHA = 8192, 48, 0.2
+N, FRAMES, ALPHA = 8192, 256, 0.2  # config 4: a batch of 256 frames x 8192 points
 
 
 def _free_port():
