@@ -368,6 +368,26 @@ def pmc_traffic(args, fmt, n, frames):
     return rec["hbm_bytes_per_launch"], f"{rec.get('source', args.traffic_file)} (librfa {sha})"
 
 
+def sq_valu(args, fmt, n, frames):
+    """roofline.valu: VALU busy fraction of the main kernel from the committed SQ-counter
+    record (SURVEY §8(d) asks for VALU busy %), used only for this exact librfa.so."""
+    from rfanalyzer_amd import _lib
+
+    try:
+        with open(os.path.join(os.path.dirname(args.traffic_file), "sq_valu.json")) as fh:
+            rec = json.load(fh).get(f"{fmt}_{n}_{frames}")
+    except (OSError, ValueError):
+        return None
+    if not rec:
+        return None
+    with open(_lib.LIB_PATH, "rb") as fh:
+        sha = hashlib.sha256(fh.read()).hexdigest()[:16]
+    if rec.get("librfa_sha16") != sha:
+        return {"busy_frac": None, "source": f"SQ record is for another build ({rec.get('librfa_sha16')}, this {sha})"}
+    return {"busy_frac": rec["valu_busy_frac"], "wave_wait_frac": rec["wave_wait_frac"],
+            "source": f"{rec['source']} (librfa {sha})"}
+
+
 # ----------------------------------------------------------------------------- cpu baseline
 def _synthetic_frames(n, frames, fmt, seed=3):
     import numpy as np
@@ -582,6 +602,9 @@ def main():
         tr, src = pmc_traffic(args, fmt, n, frames)
         result["roofline"]["traffic"] = tr
         result["roofline"]["traffic_source"] = src
+        va = sq_valu(args, fmt, n, frames)
+        if va is not None:
+            result["roofline"]["valu"] = va
         gbps, ok = copy_ceiling(torch, ranks.device)
         result["roofline"]["copy_GBps"] = gbps
         result["roofline"]["copy_kernel"] = "rfa_stream_copy (librfa float4 copy)" + ("" if ok else " MISMATCH")
