@@ -240,6 +240,14 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         A.stream = a.stream;
         hipError_t e = rfa::launch_dif_front(A);
         if (e != hipSuccess) return e;
+#ifdef RFA_DIT_FLUSH_MB
+        {  // A/B builds only: evict the scratch z from the Infinity Cache before kernel B
+            static void *flush = nullptr;
+            if (!flush && hipMalloc(&flush, (size_t)RFA_DIT_FLUSH_MB << 20) != hipSuccess) return hipErrorOutOfMemory;
+            e = hipMemsetAsync(flush, f0 & 0xff, (size_t)RFA_DIT_FLUSH_MB << 20, a.stream);
+            if (e != hipSuccess) return e;
+        }
+#endif
         FftLaunch B = a;
         B.in = reinterpret_cast<const uint8_t *>(h->d_dit_y);
         B.frame_stride = (long long)n * (long long)sizeof(float2);
