@@ -67,6 +67,14 @@ struct rfa_handle {
     float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
     int state_chunks = 1;
     int state_fused = 1;              // RFA_STATE_FUSED=0: two-kernel chunked scan
+    // RFA_STATE_OVERLAP=P: a ring-resident batch runs as P frame parts; the peak /
+    // EMA update of part p runs on state_stream beside the FFT of part p + 1
+    int state_overlap = 0;
+    bool state_lazy = false;          // RFA_STATE_JOIN=lazy: join state_stream at the next entry point
+    hipStream_t state_stream = nullptr;
+    hipEvent_t ev_fft = nullptr, ev_state[2] = {nullptr, nullptr};
+    long long part_seq = 0;           // frame parts launched so far (ev_state slot = seq & 1)
+    bool state_pending = false;       // state_stream work not yet joined into stream
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -184,10 +192,24 @@ int ensure_pinned(rfa_handle *h, size_t bytes) {
     return RFA_OK;
 }
 
-int set_device(rfa_handle *h) {
+// Order the handle stream after the state-stream work of overlapped batches.
+int join_state(rfa_handle *h) {
+    if (!h->state_pending) return RFA_OK;
+    h->state_pending = false;
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_state[(h->part_seq - 1) & 1], 0));
+    return RFA_OK;
+}
+
+int set_device_nojoin(rfa_handle *h) {
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     return RFA_OK;
+}
+
+// Every entry point but rfa_process starts here: pending state work is joined first.
+int set_device(rfa_handle *h) {
+    int rc = set_device_nojoin(h);
+    return rc ? rc : join_state(h);
 }
 
 // Collect finished profiling event pairs.
@@ -549,6 +571,21 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (h->state_chunks > 1 &&
             hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
             return bail(RFA_ERR_NOMEM);
+        if (const char *d = std::getenv("RFA_STATE_OVERLAP")) h->state_overlap = std::max(0, std::min(16, std::atoi(d)));
+        if (const char *d = std::getenv("RFA_STATE_JOIN")) h->state_lazy = std::string(d) == "lazy";
+        if (h->state_overlap >= 2 && h->d_ring) {
+            // RFA_STATE_PRIO=1: the state stream at the lowest priority, so the dispatcher
+            // prefers the FFT's whole-CU workgroups when a CU frees up
+            int lo = 0, hi = 0;
+            const char *pr = std::getenv("RFA_STATE_PRIO");
+            if (pr && std::atoi(pr) && hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+            if (hipStreamCreateWithPriority(&h->state_stream, hipStreamNonBlocking, pr && std::atoi(pr) ? lo : 0) !=
+                    hipSuccess ||
+                hipEventCreateWithFlags(&h->ev_fft, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&h->ev_state[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&h->ev_state[1], hipEventDisableTiming) != hipSuccess)
+                return bail(RFA_ERR_HIP);
+        }
     }
     if (hipMalloc(&h->d_boxcar, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (clear_ring(h) || reset_peaks_ema(h)) return bail(RFA_ERR_HIP);
@@ -561,6 +598,12 @@ int rfa_destroy(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->state_stream) {
+        hipStreamSynchronize(h->state_stream);
+        hipStreamDestroy(h->state_stream);
+    }
+    for (hipEvent_t e : {h->ev_fft, h->ev_state[0], h->ev_state[1]})
+        if (e) hipEventDestroy(e);
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     hipFree(h->d_stamps);
@@ -603,12 +646,14 @@ const char *rfa_last_error(const rfa_handle *h) { return h ? h->err.c_str() : "n
 
 int rfa_set_stream(rfa_handle *h, void *stream) {
     if (!h) return RFA_ERR_INVALID;
+    if (int rc = set_device(h)) return rc;  // pending state work joins the old stream
     h->stream = (hipStream_t)stream;
     return RFA_OK;
 }
 
 int rfa_use_own_stream(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
+    if (int rc = set_device(h)) return rc;
     h->stream = h->own_stream;
     return RFA_OK;
 }
@@ -670,7 +715,8 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     if (n_frames > (size_t)0x7fffffff) return fail(h, RFA_ERR_INVALID, "too many frames");
     if (n_frames == 0) return RFA_OK;
     if (h->pending_ring_rows >= 0) {
-        int rc = apply_ring_resize(h);
+        int rc = join_state(h);  // the resize reads the ring on the handle stream
+        if (!rc) rc = apply_ring_resize(h);
         if (rc) return rc;
     }
     const bool need_state = h->d_peaks || h->d_ema;
@@ -717,9 +763,61 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
         a.ring_logrs = h->ring_logrs;
     }
-    int rc = launch_main(h, a);
-    if (rc) return rc;
-    if (need_state || need_chan) {
+    // Overlapped form (RFA_STATE_OVERLAP=P): the batch runs as P frame parts of at
+    // most R/2 frames; part p's peak / EMA update runs on state_stream while the FFT
+    // of part p + 1 runs on the handle stream.  The FFT of part q only has to wait
+    // for the state update of part q - 2: parts q - 1 and q together hold at most R
+    // frames, so part q never overwrites a ring row that part q - 1's update reads.
+    const int n_parts = h->state_overlap;
+    const int part_len = n_parts >= 2 ? (int)((n_frames + n_parts - 1) / n_parts) : 0;
+    const bool overlap = rows_in_ring && need_state && !need_chan && h->state_stream && n_parts >= 2 &&
+                         part_len >= 32 && 2 * part_len <= h->ring_rows;
+    if (overlap) {
+        const long long R = h->ring_rows;
+        for (int f0 = 0; f0 < (int)n_frames; f0 += part_len) {
+            const int cnt = std::min<int>(part_len, (int)n_frames - f0);
+            const int base = (int)((((long long)h->write_index - f0) % R + R) % R);
+            const long long q = h->part_seq;
+            if (q >= 2) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_state[q & 1], 0));
+            FftLaunch p = a;
+            p.in = a.in + (size_t)f0 * stride;
+            p.n_frames = cnt;
+            p.ring_base = base;
+            p.ring_first = 0;
+            int rc = launch_main(h, p);
+            if (rc) return rc;
+            HIPCHK(h, hipEventRecord(h->ev_fft, h->stream));
+            HIPCHK(h, hipStreamWaitEvent(h->state_stream, h->ev_fft, 0));
+            rfa::StateLaunch s;
+            s.n = n;
+            s.n_frames = cnt;
+            s.peaks = h->d_peaks;
+            s.ema = h->d_ema;
+            s.ema_alpha = h->cfg.ema_alpha;
+            s.part = h->d_state_part;
+            s.max_chunks = h->state_chunks;
+            s.fused = h->state_fused;
+            s.stream = h->state_stream;
+            s.rows = h->d_ring;
+            s.ring_rows = h->ring_rows;
+            s.ring_base = base;
+            s.ring_logrs = h->ring_logrs;
+            HIPCHK(h, rfa::launch_state(s));
+            HIPCHK(h, hipEventRecord(h->ev_state[q & 1], h->state_stream));
+            h->part_seq = q + 1;
+            h->state_pending = true;
+        }
+        if (!h->state_lazy) {
+            int rc = join_state(h);
+            if (rc) return rc;
+        }
+    } else {
+        int rc = join_state(h);  // a lazy overlapped batch before this one
+        if (rc) return rc;
+        rc = launch_main(h, a);
+        if (rc) return rc;
+    }
+    if ((need_state || need_chan) && !overlap) {
         rfa::StateLaunch s;
         s.n = n;
         s.n_frames = (int)n_frames;
@@ -741,7 +839,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         }
         if (need_state) HIPCHK(h, rfa::launch_state(s));
         if (need_chan) {
-            rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, n_frames * sizeof(float));
+            int rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, n_frames * sizeof(float));
             if (rc) return rc;
             HIPCHK(h, rfa::launch_channel_mean(s, chan_first, chan_last, h->d_chan));
             h->chan_count = n_frames;
@@ -763,7 +861,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
 
 int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows) {
     if (!h || (!in && n_frames)) return RFA_ERR_INVALID;
-    int rc = set_device(h);
+    int rc = set_device_nojoin(h);  // process_impl joins (or overlaps) itself
     if (rc) return rc;
     return process_impl(h, in, n_frames, frame_stride_bytes, rows, h->d_window, h->cfg.input_format);
 }
@@ -789,6 +887,8 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
     if (rc) return rc;
     if (rows)
         HIPCHK(h, hipMemcpyAsync(rows, d_rows, n_frames * (size_t)h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    rc = join_state(h);
+    if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
 }

@@ -232,6 +232,36 @@ def test_config3_state_at_size(rfa, n, ring_rows, batches):
                 assert np.all(ring[[(-g) % ring_rows for g in range(f, ring_rows)]] == -9999)
 
 
+@pytest.mark.parametrize("parts,join,groups", [
+    (2, "eager", ((137,), (100,), (400,), (500,))),
+    (2, "lazy", ((137, 100), (400, 500, 250))),   # back-to-back batches, joined at the reads
+    (4, "lazy", ((500, 500), (63, 300))),        # 4 parts of 125 / 75; 63 runs unsplit (parts < 32)
+])
+def test_config3_state_overlap(rfa, monkeypatch, parts, join, groups):
+    """RFA_STATE_OVERLAP: the ring-resident batch as frame parts whose peak / EMA update
+    runs on a second stream beside the next part's FFT (engine.hip process_impl).  Same
+    ring / peaks / EMA as the restatement, with lazy joins across consecutive batches."""
+    monkeypatch.setenv("RFA_STATE_OVERLAP", str(parts))
+    monkeypatch.setenv("RFA_STATE_JOIN", join)
+    n, ring_rows, alpha = 65536, 500, 0.1
+    data, rows = _cfg3_rows(n, 1400, 5)  # one oracle pass shared by the three cases
+    fb = 2 * n
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=alpha, peak_hold=True,
+                            ring_rows=ring_rows) as e:
+        e.set_tuning(433_920_000, 20_000_000)
+        f = 0
+        for g in groups:
+            for b in g:
+                e.process(data[f * fb:(f + b) * fb], b, rows=False)
+                f += b
+            assert gu.db_diff(e.peaks(), rows[:f].max(0)) <= gu.DB_TOL, (g, f)
+            assert gu.db_diff(e.ema(), processor.ema_batch(rows[:f], alpha)) <= gu.DB_TOL, (g, f)
+            ring, ri, wi = e.ring()
+            assert ri == (-(f - 1)) % ring_rows and wi == (-f) % ring_rows
+            live = list(range(max(0, f - ring_rows), f))
+            assert gu.db_diff(ring[[(-g_) % ring_rows for g_ in live]], rows[live]) <= gu.DB_TOL
+
+
 # ---------------------------------------------------------------- waterfall speed / FFT size change
 @pytest.mark.parametrize("sizes", [(5, 8), (8, 3), (5, 5, 2, 7)])
 def test_ring_resize_keeps_history(rfa, sizes):
