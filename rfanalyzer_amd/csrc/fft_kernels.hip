@@ -19,6 +19,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "fft_common.h"
 #include "fft_kernels.h"
@@ -425,6 +426,69 @@ __global__ void state_kernel(StateLaunch a) {
     if (a.ema) a.ema[bin] = em;
 }
 
+// The same sequential recursion for a ring in column order with RS = 2^lr >= 8
+// residue blocks (N >= 256 K): storage position s*M + q holds natural bin q*RS + s,
+// so a thread walking storage order would touch peaks / EMA RS floats apart (one
+// cache line per lane).  A workgroup takes the tile q in [q0, q0 + 64) of the
+// eight blocks s in [s0, s0 + 8): its row loads stay 256-B coalesced (lane = q),
+// and its natural bins are 64 runs of 8 consecutive bins (q*RS + s0 ...), moved
+// through LDS (pitch 9, bank conflict free) in and out.  Thread (w = wave,
+// l = lane) owns blocks s0 + w and s0 + w + 4.
+template <int LR>
+__global__ void __launch_bounds__(256) state_tile_kernel(StateLaunch a) {
+    constexpr int RS = 1 << LR, SB = 8, SPT = SB / 4, TILE = 64 * SB;
+    __shared__ float pk_l[64 * (SB + 1)], em_l[64 * (SB + 1)];
+    const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = a.n >> LR, q0 = blockIdx.x * 64, s0 = blockIdx.y * SB;
+    for (int i = threadIdx.x; i < TILE; i += 256) {
+        const size_t g = (size_t)(q0 + i / SB) * RS + s0 + i % SB;  // natural bin
+        const int li = (i / SB) * (SB + 1) + i % SB;
+        pk_l[li] = a.peaks ? a.peaks[g] : 0.f;
+        em_l[li] = a.ema ? a.ema[g] : 0.f;
+    }
+    __syncthreads();
+    float pk[SPT], em[SPT];
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        pk[j] = pk_l[l * (SB + 1) + w + 4 * j];
+        em[j] = em_l[l * (SB + 1) + w + 4 * j];
+    }
+    const float al = a.ema_alpha;
+    constexpr int FR = 8;  // frames whose loads are in flight together
+    for (int f0 = 0; f0 < a.n_frames; f0 += FR) {
+        float x[FR][SPT];
+#pragma unroll
+        for (int k = 0; k < FR; k++) {
+            if (f0 + k < a.n_frames) {
+                const float *row = state_row(a, f0 + k);
+#pragma unroll
+                for (int j = 0; j < SPT; j++) x[k][j] = row[(size_t)(s0 + w + 4 * j) * m + q0 + l];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < FR; k++) {
+            if (f0 + k >= a.n_frames) break;
+#pragma unroll
+            for (int j = 0; j < SPT; j++) {
+                pk[j] = fmaxf(pk[j], x[k][j]);
+                em[j] = (em[j] > -INFINITY) ? em[j] + al * (x[k][j] - em[j]) : x[k][j];
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        pk_l[l * (SB + 1) + w + 4 * j] = pk[j];
+        em_l[l * (SB + 1) + w + 4 * j] = em[j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < TILE; i += 256) {
+        const size_t g = (size_t)(q0 + i / SB) * RS + s0 + i % SB;
+        const int li = (i / SB) * (SB + 1) + i % SB;
+        if (a.peaks) a.peaks[g] = pk_l[li];
+        if (a.ema) a.ema[g] = em_l[li];
+    }
+}
+
 // Chunked form of the same recursions for large batches: blockIdx.y = chunk of
 // chunk_len frames.  Per (chunk, bin) it stores
 //   x: max over the chunk,
@@ -531,9 +595,21 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     }
 }
 
+static const bool kStateTileOff = std::getenv("RFA_STATE_TILE") && std::atoi(std::getenv("RFA_STATE_TILE")) == 0;
+
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
     const int tpb = 256;
+    if (a.ring_rows > 0 && a.ring_logrs >= 3 && a.ring_logrs <= 5 && !kStateTileOff) {
+        // column-order ring (N >= 256 K): tiled sequential update (RFA_STATE_TILE=0: A/B off)
+        const int m = a.n >> a.ring_logrs;
+        if (m % 64 == 0) {
+            auto k = a.ring_logrs == 5 ? state_tile_kernel<5> : a.ring_logrs == 4 ? state_tile_kernel<4>
+                                                                                  : state_tile_kernel<3>;
+            hipLaunchKernelGGL(k, dim3(m / 64, (1 << a.ring_logrs) / 8), dim3(256), 0, a.stream, a);
+            return hipGetLastError();
+        }
+    }
     const int bx = (a.n + tpb - 1) / tpb;
     int chunks = a.part ? std::min(a.max_chunks, (a.n_frames + 7) / 8) : 1;
     if (chunks >= 8 && a.fused) {  // single-launch form: CH = 8, 16 or 32 chunks

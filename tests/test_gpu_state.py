@@ -262,6 +262,26 @@ def test_config3_state_overlap(rfa, monkeypatch, parts, join, groups):
             assert gu.db_diff(ring[[(-g_) % ring_rows for g_ in live]], rows[live]) <= gu.DB_TOL
 
 
+@pytest.mark.parametrize("n,batches", [(262144, (3, 9, 2)), (524288, (5, 6)), (1048576, (1, 7, 4))])
+def test_column_order_ring_state_tiles(rfa, n, batches):
+    """N >= 256 K keeps the ring in column order (RS = N / 32 K blocks); the peak / EMA
+    update reads it through state_tile_kernel (fft_kernels.hip), whose tiles move the
+    natural-order peaks / EMA through LDS.  Ring of 8 rows, so the batches wrap it."""
+    total, ring_rows, alpha = sum(batches), 8, 0.3
+    data, rows = _cfg3_rows(n, total, 21)
+    fb = 2 * n
+    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=alpha, peak_hold=True,
+                            ring_rows=ring_rows) as e:
+        assert e.ring_order == n // 32768
+        e.set_tuning(433_920_000, 250_000_000)
+        f = 0
+        for b in batches:
+            e.process(data[f * fb:(f + b) * fb], b, rows=False)
+            f += b
+            assert gu.db_diff(e.peaks(), rows[:f].max(0)) <= gu.DB_TOL, (b, f)
+            assert gu.db_diff(e.ema(), processor.ema_batch(rows[:f], alpha)) <= gu.DB_TOL, (b, f)
+
+
 # ---------------------------------------------------------------- waterfall speed / FFT size change
 @pytest.mark.parametrize("sizes", [(5, 8), (8, 3), (5, 5, 2, 7)])
 def test_ring_resize_keeps_history(rfa, sizes):
