@@ -634,24 +634,25 @@ hipError_t launch_state(const StateLaunch &a) {
     return hipGetLastError();
 }
 
-// FftProcessor.kt:143-157: mean of the channel's dB bins, one workgroup per frame.
-__global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int first, int last, float *out) {
-    const int f = blockIdx.x;
+// FftProcessor.kt:143-157: mean of the channel's dB bins, one lane per frame.  The
+// sum runs sequentially in fp32 in bin order like the reference loop (:150-152),
+// so a frame's mean is bit-exact with that loop over the same row; its latency is
+// one dependent add per bin (channels are narrow: 838 bins for 200 kHz at 1 M /
+// 250 Msps), the bins' loads are independent and pipelined.
+__global__ void __launch_bounds__(64) channel_mean_kernel(StateLaunch a, int first, int last, float *out) {
+    const int f = blockIdx.x * 64 + threadIdx.x;
+    if (f >= a.n_frames) return;
     const float *row = state_row(a, f);
     const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
     float s = 0.0f;
-    for (int i = first + (int)threadIdx.x; i < last; i += 256) s += row[ring_pos(i, lr, lm)];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    __shared__ float part[4];
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) out[f] = (part[0] + part[1] + part[2] + part[3]) / (float)(last - first);
+#pragma unroll 8
+    for (int i = first; i < last; i++) s += row[ring_pos(i, lr, lm)];
+    out[f] = s / (float)(last - first);
 }
 
 hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out) {
     if (a.n_frames <= 0 || last <= first) return hipSuccess;
-    hipLaunchKernelGGL(channel_mean_kernel, dim3(a.n_frames), dim3(256), 0, a.stream, a, first, last, out);
+    hipLaunchKernelGGL(channel_mean_kernel, dim3((a.n_frames + 63) / 64), dim3(64), 0, a.stream, a, first, last, out);
     return hipGetLastError();
 }
 

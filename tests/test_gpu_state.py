@@ -164,17 +164,26 @@ def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
     ref_rows = oracle.spectrum_rows(data, oracle.IN_S8, n, frames, None, oracle.WIN_BLACKMAN)
     exp = [processor.channel_mean(r, n, freq, sr, *chan) for r in ref_rows]
     # 64 K: the batch fits the ring, so the means read the residue-major ring rows;
-    # the other sizes read the staging rows (batch larger than the ring)
+    # the other sizes read the caller rows (batch larger than the ring)
     with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=12 if n == 65536 else 8) as e:
         e.set_tuning(freq, sr)
         e.set_channel(*chan)
-        e.process(data, frames, rows=False)
+        if n == 65536:
+            e.process(data, frames, rows=False)
+            ring, _, _ = e.ring()
+            gpu_rows = ring[[(-g) % 12 for g in range(frames)]]
+        else:
+            gpu_rows = e.process(data, frames)
         got = e.channel_means()
     if exp[0] is None:
         assert got.size == 0
         return
     assert got.size == frames
     np.testing.assert_allclose(got, np.array(exp, np.float32), rtol=0, atol=gu.DB_TOL)
+    # the reference's own loop (sequential fp32 sum, :150-152) over the rows the GPU
+    # produced gives the GPU's means bit for bit
+    same = [processor.channel_mean(r, n, freq, sr, *chan) for r in gpu_rows]
+    np.testing.assert_array_equal(got, np.array(same, np.float32))
 
 
 # ---------------------------------------------------------------- config 3 at its real size
