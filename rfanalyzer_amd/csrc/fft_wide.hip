@@ -86,39 +86,43 @@ template <typename T>
 __device__ __forceinline__ T *lds_opaque(T *p) { return p; }  // host pass: never executed
 #endif
 
-template <int Q, int LOGM, int PT>
+template <int Q, int LOGM, int PT, int KR = 2>
 __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
+    // KR rounds (2: the M/2 buffer; 4: an M/4 buffer, RFA_SPLIT_STAGE) -- round h
+    // moves the outputs landing in [h*M/KR, (h+1)*M/KR) and the inputs t' in
+    // [h*R'/KR, (h+1)*R'/KR), which come from the same part
     using G = WGeo<LOGM, PT>;
     using W = WPass<Q, LOGM, PT>;
     using N = WPass<Q + 1, LOGM, PT>;
-    static_assert(N::R >= 2, "half-round split needs radix >= 2");
-    float2 in[2][PT / 2];
+    static_assert(N::R >= KR && (W::NB == 1 || W::NB % KR == 0), "round split needs radix >= KR");
+    constexpr int PART = G::M / KR, PARTP = PART + PART / 32;
+    float2 in[KR][PT / KR];
     const int wk = tid & (W::P - 1);
     const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
     const int rbase = padw(tid);                     // butterfly b adds TPF*b
-    const int my_half = tid >= G::TPF / 2;           // NB == 1 writers only
+    const int my_part = tid / (G::TPF / KR);         // NB == 1 writers only
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
+    for (int h = 0; h < KR; h++) {
         if constexpr (W::NB == 1) {
-            if (my_half == h) {
+            if (my_part == h) {
 #pragma unroll
-                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * (G::HALFP)] = v[t];
+                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
             }
         } else {
 #pragma unroll
-            for (int b = h * W::NB / 2; b < (h + 1) * W::NB / 2; b++) {
+            for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
 #pragma unroll
                 for (int t = 0; t < W::R; t++)
-                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * G::HALF)] = v[b * W::R + t];
+                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * PART)] = v[b * W::R + t];
             }
         }
         lds_barrier();
 #pragma unroll
         for (int b = 0; b < N::NB; b++) {
 #pragma unroll
-            for (int t = h * N::R / 2; t < (h + 1) * N::R / 2; t++)
-                in[h][b * (N::R / 2) + (t - h * N::R / 2)] =
-                    buf[rbase + padw(G::TPF * b + t * N::STRIDE - h * G::HALF)];
+            for (int t = h * N::R / KR; t < (h + 1) * N::R / KR; t++)
+                in[h][b * (N::R / KR) + (t - h * N::R / KR)] =
+                    buf[rbase + padw(G::TPF * b + t * N::STRIDE - h * PART)];
         }
         lds_barrier();
     }
@@ -126,8 +130,8 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     for (int b = 0; b < N::NB; b++) {
 #pragma unroll
         for (int t = 0; t < N::R; t++) {
-            const int h = t >= N::R / 2;
-            v[b * N::R + t] = in[h][b * (N::R / 2) + (t - h * N::R / 2)];
+            const int h = t / (N::R / KR);
+            v[b * N::R + t] = in[h][b * (N::R / KR) + (t - h * N::R / KR)];
         }
     }
 }
@@ -204,6 +208,13 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // are adjacent in the interleaved window (one 8/16-byte load).  Loads run one
 // chunk ahead of the arithmetic (software pipeline), so a wave keeps two
 // chunks of L2 requests in flight instead of waiting a full round trip per chunk.
+// 64 K, 8-bit input: stage the next frame in two halves, the first right after the
+// pre-stage (exchanges then run in four rounds through a quarter buffer).  1 = on
+// (default, -1..-4 % kernel time, profiles/r02g/split_stage_ab.txt), 0 = whole frame
+// after exchange 1, 2 = first half after exchange 0 (+10 %, not kept).
+#ifndef RFA_SPLIT_STAGE
+#define RFA_SPLIT_STAGE 1
+#endif
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
@@ -217,7 +228,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // PADRAW (fft_w64_kernel): the staged frame sits in LDS as 8 KiB pieces at a
 // 8448-B pitch (one piece per wave region), i.e. raw element e at e + (e >> 12) * 128.
 template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0,
-          bool PADRAW = false>
+          bool PADRAW = false, int JS = 0>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
                                          const float2 *wpre = nullptr) {
@@ -256,7 +267,8 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG) {  // frame staged in LDS
-                    const int e = mo + j * M;
+                    // JS != 0 (RFA_SPLIT_STAGE): the frame's halves sit JS raw elements apart
+                    const int e = mo + j * (JS != 0 ? JS : M);
                     raw[s][q][j] = lraw_t[PADRAW ? e + (e >> 12) * 128 : e];
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
@@ -415,7 +427,26 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
-    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & ~48) == 0 &&
+#ifdef RFA_DIAG_STG12  // A/B builds only: the staged kernel without butterflies / exchanges (DIAG 12)
+    constexpr int STG_DIAG_OK = ~60;
+#else
+    constexpr int STG_DIAG_OK = ~48;
+#endif
+    // RFA_SPLIT_STAGE (A/B builds; RS = 2, 8-bit input): the exchanges run in four
+    // rounds through the buffer's first M/4 region A, so the next frame's first half
+    // is staged into region B right after this item's pre-stage (it flies during both
+    // exchanges and passes) and only its second half waits for exchange 1 (into A).
+    constexpr bool SPLIT = RFA_SPLIT_STAGE && STG && RS == 2 && LOGM == 15 && BPS == 2 && !COMPLEX_OUT;
+    // RFA_SPLIT_STAGE=2: exchange 0 keeps two rounds over the whole buffer and the
+    // first half is staged after it (fewer barriers, less time in flight)
+    constexpr bool SPLIT_LATE = SPLIT && RFA_SPLIT_STAGE == 2;
+    constexpr int KR = SPLIT ? 4 : 2;                 // exchange rounds (exchange 1; exchange 0 too unless SPLIT_LATE)
+    constexpr int KR0 = SPLIT_LATE ? 2 : KR;
+    constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
+    constexpr int HALF_BYTES = M * RS * BPS / 2;
+    constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
+    static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
+    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
@@ -451,10 +482,22 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         __syncthreads();  // every wave has read the slot before it is rewritten
     }
     auto next_item = [&](int u) { return u + (int)gridDim.x; };
+    // SPLIT: half 0 of a frame goes to region B, half 1 to region A
+    auto stage_half = [&](int f, int half) {
+        if constexpr (SPLIT)
+            stage_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0),
+                                                half ? buf : buf + QP);
+    };
     if constexpr (STG) {
         const int f0 = frame_of(u0);
-        if (u0 < items && f0 < a.n_frames)
-            stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
+        if (u0 < items && f0 < a.n_frames) {
+            if constexpr (SPLIT) {
+                stage_half(f0, 0);
+                stage_half(f0, 1);
+            } else {
+                stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
+            }
+        }
     }
 
     // One work item (SLOTS frames, or one residue of a frame).  Between items no
@@ -522,7 +565,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
         using RawT = typename Raw<FMT>::T;
-        const RawT *lraw = reinterpret_cast<const RawT *>(buf);
+        const RawT *lraw = reinterpret_cast<const RawT *>(SPLIT ? buf + QP : buf);
         if constexpr (STG) {
             // this item's frame, staged by LDS-DMA during the previous item: wait for
             // this wave's pieces, then for every wave's (the barrier)
@@ -559,7 +602,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP>(v, a.window_il, a.wide_tw, in_rs,
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP, false, JS>(v, a.window_il, a.wide_tw, in_rs,
                                                                                         tid, planar, lraw, wpre)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
@@ -575,18 +618,28 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if (dq && threadIdx.x == 0) qslot[0] = dequeue();
             lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
             if (dq) unext = qslot[0];
+            if constexpr (SPLIT && !SPLIT_LATE) {  // region B is free until the next item: its half of the next frame now
+                const int fn = frame_of(unext);
+                if (unext < items && fn < a.n_frames) stage_half(fn, 0);
+            }
         }
-        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT>(v, buf, tid);
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR0>(v, buf, tid);
+        if constexpr (SPLIT_LATE) {  // exchange 0 ended with a barrier after its last reads
+            const int fn = frame_of(unext);
+            if (unext < items && fn < a.n_frames) stage_half(fn, 0);
+        }
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
-        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT>(v, buf, tid);
+        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
         stamp(u, 4);
         if constexpr (STG) {
             // exchange 1 ended with a barrier after its last reads: the buffer is free
             // until the next item, so stage the next item's frame now
             const int fn = frame_of(unext);
-            if (unext < items && fn < a.n_frames)
-                stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
+            if (unext < items && fn < a.n_frames) {
+                if constexpr (SPLIT) stage_half(fn, 1);
+                else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
+            }
         }
         if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
         stamp(u, 5);
@@ -1071,6 +1124,12 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         if (a.fmt != 0 || co) return hipErrorInvalidValue;
         return launch_wide_one<15, 32, 2, 0, false, 16, true>(a);
     }
+#ifdef RFA_DIAG_STG12
+    if (a.diag == 12 && a.logn == 16) {  // staged 64 K kernel, streaming part only (A/B builds)
+        if (a.fmt != 0 || co) return hipErrorInvalidValue;
+        return launch_wide_one<15, 32, 2, 0, false, 12, true>(a);
+    }
+#endif
     if (a.diag == 32) {  // phase stamps of the staged s8 kernels (profiling only)
         if (a.fmt != 0 || co || !a.stamps) return hipErrorInvalidValue;
         switch (a.logn) {
