@@ -215,6 +215,12 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_SPLIT_STAGE
 #define RFA_SPLIT_STAGE 1
 #endif
+// 8/16 K ... 32 K one-residue kernels, 8-bit input: with the exchanges in four rounds
+// through region A the whole next frame fits region B and is staged right after the
+// pre-stage (RFA_SPLIT_WHOLE=1).
+#ifndef RFA_SPLIT_WHOLE
+#define RFA_SPLIT_WHOLE 0
+#endif
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
@@ -440,9 +446,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // RFA_SPLIT_STAGE=2: exchange 0 keeps two rounds over the whole buffer and the
     // first half is staged after it (fewer barriers, less time in flight)
     constexpr bool SPLIT_LATE = SPLIT && RFA_SPLIT_STAGE == 2;
-    constexpr int KR = SPLIT ? 4 : 2;                 // exchange rounds (exchange 1; exchange 0 too unless SPLIT_LATE)
-    constexpr int KR0 = SPLIT_LATE ? 2 : KR;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
+    constexpr bool WHOLE_B = RFA_SPLIT_WHOLE && STG && RS == 1 && LOGM >= 14 && BPS == 2 && !COMPLEX_OUT &&
+                             M * BPS <= (G::HALFP - QP) * 8;
+    constexpr int KR = (SPLIT || WHOLE_B) ? 4 : 2;   // exchange rounds (exchange 1; exchange 0 too unless SPLIT_LATE)
+    constexpr int KR0 = SPLIT_LATE ? 2 : KR;
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
@@ -488,10 +496,15 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             stage_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0),
                                                 half ? buf : buf + QP);
     };
+    auto stage_b = [&](int f) {  // WHOLE_B: the whole frame into region B
+        if constexpr (WHOLE_B) stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride, buf + QP);
+    };
     if constexpr (STG) {
         const int f0 = frame_of(u0);
         if (u0 < items && f0 < a.n_frames) {
-            if constexpr (SPLIT) {
+            if constexpr (WHOLE_B) {
+                stage_b(f0);
+            } else if constexpr (SPLIT) {
                 stage_half(f0, 0);
                 stage_half(f0, 1);
             } else {
@@ -565,7 +578,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
         using RawT = typename Raw<FMT>::T;
-        const RawT *lraw = reinterpret_cast<const RawT *>(SPLIT ? buf + QP : buf);
+        const RawT *lraw = reinterpret_cast<const RawT *>((SPLIT || WHOLE_B) ? buf + QP : buf);
         if constexpr (STG) {
             // this item's frame, staged by LDS-DMA during the previous item: wait for
             // this wave's pieces, then for every wave's (the barrier)
@@ -622,6 +635,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 const int fn = frame_of(unext);
                 if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
+            if constexpr (WHOLE_B) {  // region B is free until the next item: the whole next frame now
+                const int fn = frame_of(unext);
+                if (unext < items && fn < a.n_frames) stage_b(fn);
+            }
         }
         if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR0>(v, buf, tid);
         if constexpr (SPLIT_LATE) {  // exchange 0 ended with a barrier after its last reads
@@ -638,7 +655,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             const int fn = frame_of(unext);
             if (unext < items && fn < a.n_frames) {
                 if constexpr (SPLIT) stage_half(fn, 1);
-                else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
+                else if constexpr (!WHOLE_B) stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
         if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
