@@ -211,7 +211,8 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // 64 K, 8-bit input: stage the next frame in two halves, the first right after the
 // pre-stage (exchanges then run in four rounds through a quarter buffer).  1 = on
 // (default, -1..-4 % kernel time, profiles/r02g/split_stage_ab.txt), 0 = whole frame
-// after exchange 1, 2 = first half after exchange 0 (+10 %, not kept).
+// after exchange 1, 2 = first half after exchange 0 (+10 %, not kept), 3 = second half
+// loaded directly by the pre-stage (+5..8 %, not kept, split_direct_ab.txt).
 #ifndef RFA_SPLIT_STAGE
 #define RFA_SPLIT_STAGE 1
 #endif
@@ -234,7 +235,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // PADRAW (fft_w64_kernel): the staged frame sits in LDS as 8 KiB pieces at a
 // 8448-B pitch (one piece per wave region), i.e. raw element e at e + (e >> 12) * 128.
 template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0,
-          bool PADRAW = false, int JS = 0>
+          bool PADRAW = false, int JS = 0, bool HI_DIRECT = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
                                          const float2 *wpre = nullptr) {
@@ -273,9 +274,13 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG) {  // frame staged in LDS
-                    // JS != 0 (RFA_SPLIT_STAGE): the frame's halves sit JS raw elements apart
-                    const int e = mo + j * (JS != 0 ? JS : M);
-                    raw[s][q][j] = lraw_t[PADRAW ? e + (e >> 12) * 128 : e];
+                    if (HI_DIRECT && j >= 1) {  // RFA_SPLIT_STAGE=3: the second half straight from memory
+                        raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
+                    } else {
+                        // JS != 0 (RFA_SPLIT_STAGE): the frame's halves sit JS raw elements apart
+                        const int e = mo + j * (JS != 0 ? JS : M);
+                        raw[s][q][j] = lraw_t[PADRAW ? e + (e >> 12) * 128 : e];
+                    }
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
@@ -446,6 +451,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // RFA_SPLIT_STAGE=2: exchange 0 keeps two rounds over the whole buffer and the
     // first half is staged after it (fewer barriers, less time in flight)
     constexpr bool SPLIT_LATE = SPLIT && RFA_SPLIT_STAGE == 2;
+    // RFA_SPLIT_STAGE=3: only the first half is staged (early); the pre-stage loads the
+    // second half straight from memory (no late DMA to wait for)
+    constexpr bool SPLIT_DIRECT = SPLIT && RFA_SPLIT_STAGE == 3;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
     constexpr bool WHOLE_B = RFA_SPLIT_WHOLE && STG && RS == 1 && LOGM >= 14 && BPS == 2 && !COMPLEX_OUT &&
                              M * BPS <= (G::HALFP - QP) * 8;
@@ -506,7 +514,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 stage_b(f0);
             } else if constexpr (SPLIT) {
                 stage_half(f0, 0);
-                stage_half(f0, 1);
+                if constexpr (!SPLIT_DIRECT) stage_half(f0, 1);
             } else {
                 stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
             }
@@ -615,7 +623,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP, false, JS>(v, a.window_il, a.wide_tw, in_rs,
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP, false, JS, SPLIT_DIRECT>(v, a.window_il, a.wide_tw, in_rs,
                                                                                         tid, planar, lraw, wpre)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
@@ -654,7 +662,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // until the next item, so stage the next item's frame now
             const int fn = frame_of(unext);
             if (unext < items && fn < a.n_frames) {
-                if constexpr (SPLIT) stage_half(fn, 1);
+                if constexpr (SPLIT) {
+                    if constexpr (!SPLIT_DIRECT) stage_half(fn, 1);
+                }
                 else if constexpr (!WHOLE_B) stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
