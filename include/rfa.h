@@ -133,6 +133,25 @@ RFA_API int rfa_synchronize(rfa_handle *h);
 RFA_API int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 RFA_API int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 
+/* Scheduler.run's FFT branch, one raw packet at a time (Scheduler.kt:252-273
+ * with the converters' fillPacketIntoSamplePacket, Signed8BitIQConverter.java:80-98,
+ * Unsigned8BitIQConverter.java:80-98, Signed16BitIQConverter.kt:89-124): the
+ * packet's whole samples (host bytes in the handle's input format) fill the
+ * handle's partial frame from the packet start at startIndex = samples already
+ * held; once it holds N samples the frame is processed like rfa_process_host
+ * (ring, peaks, EMA, channel mean) after rfa_set_tuning(frequency, sample_rate)
+ * of the packet that completed it, and the rest of that packet is dropped.  So
+ * P-sample packets give one frame per packet when P >= N and one frame every
+ * ceil(N / P) packets when P < N (e.g. RTL-SDR's 16 KiB = 8192-sample packets,
+ * RtlsdrSource.java:112, at the default N = 16384).  *frames = 1 when a frame
+ * was processed (its row copied to row_out, N floats, unless NULL), else 0.
+ * Synchronous.  RFA_ERR_UNSUPPORTED for RFA_IN_F32_PLANAR.  rfa_reset_state and
+ * rfa_set_fft_size discard a partial frame (Scheduler.kt:259-260);
+ * rfa_pending_samples reports how many samples it holds. */
+RFA_API int rfa_push_packet(rfa_handle *h, const void *packet, size_t packet_bytes, int64_t frequency,
+                            int64_t sample_rate, float *row_out, int32_t *frames);
+RFA_API int rfa_pending_samples(const rfa_handle *h, int64_t *samples);
+
 /* Tuning metadata of the following frames (SamplePacket.frequency/sampleRate).
  * Mirrors FftProcessor.kt:169-220,238-239: a frequency change shifts every ring
  * row by (int)((f_old-f_new)*(N/(float)sr)) bins with -9999 fill (or clears it
@@ -221,10 +240,15 @@ RFA_API int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_
 RFA_API int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, size_t count, float *peak,
                                  float *avg);
 
-/* Device-side state pointers (valid until rfa_destroy), for zero-copy consumers.
- * peaks and EMA are in natural (fft-shifted) bin order.  The ring's rows are
- * stored in the order rfa_get_ring_order reports. */
+/* Device-side state pointers, for zero-copy consumers.  peaks and EMA are in
+ * natural (fft-shifted) bin order.  The ring's rows are stored in the order
+ * rfa_get_ring_order reports.  The pointers (and the ring order) stay valid only
+ * while rfa_get_state_generation returns the same value: a retune that shifts
+ * the ring (rfa_set_tuning swaps the ring with its shift buffer), a ring resize
+ * applied by rfa_process (rfa_set_ring_rows) and rfa_set_fft_size (which rebuilds
+ * every buffer and frees the old ones) each advance it; re-query after a change. */
 RFA_API int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema);
+RFA_API int rfa_get_state_generation(const rfa_handle *h, int64_t *generation);
 
 /* Storage order of the device ring rows (no reference counterpart: the JVM
  * waterfallBuffer rows are natural order, FftProcessor.kt:222-227, and

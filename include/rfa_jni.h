@@ -55,8 +55,12 @@ JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFTAndLogMa
                                                                                    jfloatArray output);
 JNIEXPORT jboolean JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performWindowedFftAndReturnMagNative(
     JNIEnv *env, jobject thiz, jfloatArray re, jfloatArray im, jfloatArray mag_out);
-/* format: rfa_input_format; packet holds n_frames*fft frames at frame_stride bytes
- * (0 = dense); mag_out holds n_frames*fft floats.  Returns frames processed or -1. */
+/* format: rfa_input_format.  frame_stride 0: the reference's framing
+ * (Scheduler.kt:252-273) on the cached setup -- the packet fills a partial frame
+ * across calls; returns 1 with the completed frame's row in mag_out[0, fft_size)
+ * or 0 while the frame is incomplete.  frame_stride > 0: batch mode, every whole
+ * frame at frame_stride bytes that packet and mag_out hold; returns the count.
+ * -1 on error (mag_out shorter than fft_size, bad format). */
 JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processIqBytesNative(
     JNIEnv *env, jobject thiz, jbyteArray packet, jint format, jint fft_size, jint frame_stride,
     jfloatArray mag_out);
@@ -67,8 +71,12 @@ JNIEXPORT jlong JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_createAnalyzerNat
     jfloat ema_alpha, jboolean peak_hold, jint ring_rows, jint device);
 JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_destroyAnalyzerNative(JNIEnv *env, jobject thiz,
                                                                                      jlong handle);
-/* One raw packet (frames at frame_stride bytes, 0 = dense) into ring + state after
- * SamplePacket.frequency / sampleRate (rfa_set_tuning).  Returns frames or < 0. */
+/* One raw packet into ring + state.  frame_stride 0: the reference's framing
+ * (rfa_push_packet: Scheduler.kt:252-273, a partial frame filled across packets,
+ * the tuning of the completing packet); returns 1 when a frame was processed,
+ * 0 while it is incomplete.  frame_stride > 0: batch mode, every whole frame at
+ * that stride after rfa_set_tuning(frequency, sample_rate); returns the count.
+ * < 0: rfa_status. */
 JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processPacketNative(
     JNIEnv *env, jobject thiz, jlong handle, jbyteArray packet, jint frame_stride, jlong frequency,
     jlong sample_rate);

@@ -180,3 +180,35 @@ def channel_mean(row: np.ndarray, n: int, frequency: int, sample_rate: int, star
     for v in np.asarray(row[s:e], np.float32):
         acc = np.float32(acc + v)
     return np.float32(acc / np.float32(e - s))
+
+
+def scheduler_frames(packets, n: int, bytes_per_sample: int):
+    """Scheduler.run's FFT branch restated literally (Scheduler.kt:252-273 with
+    fillPacketIntoSamplePacket, Signed8BitIQConverter.java:80-98): one buffer of
+    N samples filled packet after packet from each packet's start, delivered when
+    full, the rest of the completing packet dropped; the buffer takes the
+    frequency / sample rate of every packet that fills it (the last one wins).
+    packets: iterable of (bytes, frequency, sample_rate).  Returns a list of
+    (frame_bytes, frequency, sample_rate), one per delivered frame."""
+    out = []
+    buf = bytearray()
+    size = 0
+    freq = rate = None
+    for data, f, r in packets:
+        if size >= n:  # never: a full buffer is delivered at once
+            continue
+        count = 0
+        i = 0
+        while i + bytes_per_sample <= len(data):
+            buf += data[i:i + bytes_per_sample]
+            count += 1
+            i += bytes_per_sample
+            if size + count >= n:
+                break
+        size += count
+        freq, rate = f, r
+        if size == n:
+            out.append((bytes(buf), freq, rate))
+            buf = bytearray()
+            size = 0
+    return out

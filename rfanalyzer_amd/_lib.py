@@ -93,6 +93,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_process": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_process_host": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_set_tuning": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
+        "rfa_push_packet": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, _vp,
+                                           ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_pending_samples": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int64)]),
+        "rfa_get_state_generation": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int64)]),
         "rfa_get_peaks": (ctypes.c_int, [_h, _fp]),
         "rfa_get_ema": (ctypes.c_int, [_h, _fp]),
         "rfa_get_boxcar": (ctypes.c_int, [_h, ctypes.c_int32, _fp]),

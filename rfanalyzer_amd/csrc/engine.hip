@@ -18,6 +18,7 @@
 
 #include "../../include/rfa.h"
 #include "fft_kernels.h"
+#include "framer.h"
 
 static constexpr size_t kStampWords = (size_t)2048 * 16 * 8;  // RFA_STAMPS_FILE buffer: [blocks][16][8]
 
@@ -94,6 +95,9 @@ struct rfa_handle {
     float view_min_db = 0.f, view_max_db = 0.f;
     size_t chan_count = 0;
     int64_t last_frequency = 0, last_sample_rate = 0;
+    // rfa_push_packet: the partial SamplePacket Scheduler.run fills across packets
+    rfa::PacketFramer framer;
+    int64_t generation = 0;           // rfa_get_state_generation: device state pointers changed
     // staging for host-pointer entry points / state without a row buffer
     void *d_in = nullptr;
     size_t d_in_cap = 0;
@@ -449,6 +453,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     h->logn = logn;
     h->device = cfg->device_id;
     h->ring_rows = cfg->ring_rows;
+    h->framer.configure((size_t)h->n, bytes_per_sample(cfg->input_format));
     int rc = set_device(h);
     if (rc) { delete h; return rc; }
     auto bail = [&](int code) { rfa_destroy(h); return code; };
@@ -701,6 +706,7 @@ static int apply_ring_resize(rfa_handle *h) {
     h->dirty.assign((size_t)rn, 1);  // FftProcessor.kt:193
     h->write_index = 0;
     if (h->read_index >= rn) h->read_index = 0;  // rewritten by the frame that triggered the resize
+    h->generation++;
     return RFA_OK;
 }
 
@@ -893,6 +899,29 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
     return RFA_OK;
 }
 
+int rfa_push_packet(rfa_handle *h, const void *packet, size_t packet_bytes, int64_t frequency, int64_t sample_rate,
+                    float *row_out, int32_t *frames) {
+    if (!h || !frames || (!packet && packet_bytes) || sample_rate <= 0) return RFA_ERR_INVALID;
+    *frames = 0;
+    if (h->cfg.input_format == RFA_IN_F32_PLANAR)
+        return fail(h, RFA_ERR_UNSUPPORTED, "packet framing needs an interleaved sample format");
+    if (!h->framer.push(packet, packet_bytes)) return RFA_OK;  // the frame waits for more packets
+    // complete: the tuning of the packet that completed it (Signed8BitIQConverter.java:95-96),
+    // then one frame through ring / peaks / EMA / channel mean (FftProcessor.kt:125-245)
+    int rc = rfa_set_tuning(h, frequency, sample_rate);
+    if (!rc) rc = rfa_process_host(h, h->framer.data(), 1, 0, row_out);
+    h->framer.clear();  // the next packet starts a new SamplePacket (Scheduler.kt:266-270)
+    if (rc) return rc;
+    *frames = 1;
+    return RFA_OK;
+}
+
+int rfa_pending_samples(const rfa_handle *h, int64_t *samples) {
+    if (!h || !samples) return RFA_ERR_INVALID;
+    *samples = (int64_t)h->framer.filled();
+    return RFA_OK;
+}
+
 int64_t rfa_retune_offset(int64_t frequency_diff, int n, int64_t sample_rate) {
     if (sample_rate <= 0) return 0;
     // FftProcessor.kt:143,199: (fdiff * (N / sampleRate.toFloat())).toInt(), float arithmetic
@@ -927,6 +956,7 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
                 HIPCHK(h, rfa::launch_ring_shift(h->d_ring, h->d_ring_tmp, h->ring_rows, h->n, h->ring_logrs, (int)off, kRingFill,
                                                  h->stream));
                 std::swap(h->d_ring, h->d_ring_tmp);
+                h->generation++;
                 std::fill(h->dirty.begin(), h->dirty.end(), 1);  // FftProcessor.kt:215
             } else {
                 rc = clear_ring(h);
@@ -1013,7 +1043,6 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
         if (!h->dirty[bi] && row_number > L) continue;
         if ((int)sel.size() > L + 5) break;
         sel.push_back(make_int2(row_number, bi));
-        h->dirty[bi] = 0;
     }
     // one device block: colormap | row list | averages [L+1][W] | path y | peaks y | autoscale
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1034,6 +1063,9 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
     HIPCHK(h, hipMemcpyAsync(base, p->colormap, (size_t)p->colormap_size * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->d_draw, sel.data(), sel.size() * sizeof(int2), hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, rfa::launch_draw(a));
+    // refreshed rows become clean only once their refresh is enqueued (a failed
+    // launch above leaves them dirty for the next draw)
+    for (const int2 &r : sel) h->dirty[(size_t)r.y] = 0;
     HIPCHK(h, hipMemcpyAsync(colors, a.colors, (size_t)R * W * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipMemcpyAsync(fft_path_y, a.path_y, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));
     if (peaks_y) HIPCHK(h, hipMemcpyAsync(peaks_y, a.peaks_y, (size_t)W * 4, hipMemcpyDeviceToHost, h->stream));
@@ -1150,6 +1182,7 @@ int rfa_reset_state(rfa_handle *h) {
     h->write_index = h->read_index = 0;
     h->have_rows = false;
     h->have_tuning = false;
+    h->framer.clear();
     rc = clear_ring(h);
     if (rc) return rc;
     rc = reset_peaks_ema(h);
@@ -1188,6 +1221,7 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
     nh->chan_end = h->chan_end;
     if (h->stream != h->own_stream) nh->stream = h->stream;
     nh->profile = h->profile;
+    nh->generation = h->generation + 1;
     std::swap(*h, *nh);
     rfa_destroy(nh);  // the old tables and buffers
     return RFA_OK;
@@ -1196,6 +1230,12 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
 int rfa_get_ring_order(const rfa_handle *h, int32_t *residues) {
     if (!h || !residues) return RFA_ERR_INVALID;
     *residues = 1 << h->ring_logrs;
+    return RFA_OK;
+}
+
+int rfa_get_state_generation(const rfa_handle *h, int64_t *generation) {
+    if (!h || !generation) return RFA_ERR_INVALID;
+    *generation = h->generation;
     return RFA_OK;
 }
 

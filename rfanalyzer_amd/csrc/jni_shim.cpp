@@ -89,24 +89,33 @@ JNIEXPORT jboolean JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performWindowe
 
 JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processIqBytesNative(
     JNIEnv *env, jobject, jbyteArray packet, jint format, jint fft_size, jint frame_stride, jfloatArray mag_out) {
+    if (!packet || !mag_out || fft_size <= 0 || frame_stride < 0) return -1;
     const jsize bytes = (*env)->GetArrayLength(env, packet);
     const jsize out_len = (*env)->GetArrayLength(env, mag_out);
-    if (fft_size <= 0 || frame_stride < 0 || bytes <= 0) return -1;
     static const int bps_tab[5] = {2, 2, 4, 8, 8};
-    if (format < 0 || format > 4) return -1;
-    const long long frame_bytes = (long long)fft_size * bps_tab[format];
-    const long long stride = frame_stride ? frame_stride : frame_bytes;
-    if (bytes < frame_bytes) return 0;
-    long long n_frames = (bytes - frame_bytes) / stride + 1;
-    if (n_frames * fft_size > out_len) n_frames = out_len / fft_size;
-    if (n_frames <= 0) return 0;
+    if (format < 0 || format > 4 || bytes < 0 || out_len < fft_size) return -1;
     std::lock_guard<std::mutex> lock(g_mu);
     rfa_handle *h = handle_for(fft_size, format, RFA_WINDOW_BLACKMAN);
     if (!h) return -1;
-    std::vector<jbyte> in(bytes);
+    std::vector<jbyte> in((size_t)bytes);
+    if (bytes) (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
+    if (frame_stride == 0) {
+        // the reference's framing (Scheduler.kt:252-273): the packet fills the cached
+        // setup's partial frame; a completed frame's row goes to mag_out[0, N)
+        if (format == RFA_IN_F32_PLANAR) return -1;
+        std::vector<float> row((size_t)fft_size);
+        int32_t frames = 0;
+        if (rfa_push_packet(h, in.data(), (size_t)bytes, 0, 1, row.data(), &frames) != RFA_OK) return -1;
+        if (frames) (*env)->SetFloatArrayRegion(env, mag_out, 0, fft_size, row.data());
+        return frames;
+    }
+    // batch mode: whole frames at frame_stride bytes, as many as packet and mag_out hold
+    const long long frame_bytes = (long long)fft_size * bps_tab[format];
+    if (bytes < frame_bytes) return 0;
+    long long n_frames = (bytes - frame_bytes) / frame_stride + 1;
+    if (n_frames * fft_size > out_len) n_frames = out_len / fft_size;
     std::vector<float> rows((size_t)n_frames * fft_size);
-    (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
-    if (rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)stride, rows.data()) != RFA_OK) return -1;
+    if (rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)frame_stride, rows.data()) != RFA_OK) return -1;
     (*env)->SetFloatArrayRegion(env, mag_out, 0, (jsize)rows.size(), rows.data());
     return (jint)n_frames;
 }
@@ -146,15 +155,25 @@ JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processPacketNativ
     if (rfa_get_config(h, &c) != RFA_OK) return RFA_ERR_INVALID;
     static const int bps_tab[5] = {2, 2, 4, 8, 8};
     const jsize bytes = (*env)->GetArrayLength(env, packet);
+    if (bytes < 0) return RFA_ERR_INVALID;
+    std::vector<jbyte> in((size_t)bytes);
+    if (bytes) (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
+    if (frame_stride == 0) {
+        // Scheduler.kt:252-273: the packet fills the handle's partial frame (across
+        // packets when it is shorter than a frame, the rest dropped when longer);
+        // returns 1 when a frame was completed and processed, else 0
+        int32_t frames = 0;
+        const int rc = rfa_push_packet(h, in.data(), (size_t)bytes, frequency, sample_rate, nullptr, &frames);
+        return rc != RFA_OK ? rc : frames;
+    }
+    // batch mode (no reference counterpart): every whole frame at frame_stride bytes;
+    // a partial frame of the framing mode is left pending
     const long long frame_bytes = (long long)c.fft_size * bps_tab[c.input_format];
-    const long long stride = frame_stride ? frame_stride : frame_bytes;
-    if (bytes < frame_bytes) return 0;  // a partial frame waits (Scheduler.kt:264-270 fills across packets)
-    const long long n_frames = (bytes - frame_bytes) / stride + 1;
+    if (bytes < frame_bytes) return 0;
+    const long long n_frames = (bytes - frame_bytes) / frame_stride + 1;
     int rc = rfa_set_tuning(h, frequency, sample_rate);
     if (rc != RFA_OK) return rc;
-    std::vector<jbyte> in(bytes);
-    (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
-    rc = rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)stride, nullptr);
+    rc = rfa_process_host(h, in.data(), (size_t)n_frames, (size_t)frame_stride, nullptr);
     return rc != RFA_OK ? rc : (jint)n_frames;
 }
 

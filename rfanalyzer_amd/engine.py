@@ -96,6 +96,31 @@ class SpectrumEngine:
                                                 out.ctypes.data if rows else None), "rfa_process_host")
         return out
 
+    def push_packet(self, packet, frequency: int, sample_rate: int, row: bool = False):
+        """One raw packet through the reference's framing (rfa_push_packet,
+        Scheduler.kt:252-273): fills the partial frame, processes it once complete.
+        Returns the completed frame's row (row=True) / True, or None / False."""
+        buf = _as_u8(packet)
+        out = np.empty(self.n, np.float32) if row else None
+        got = ctypes.c_int32(0)
+        self._check(_lib.lib().rfa_push_packet(self._h, buf.ctypes.data if buf.size else None, buf.size,
+                                               int(frequency), int(sample_rate),
+                                               out.ctypes.data if row else None, ctypes.byref(got)),
+                    "rfa_push_packet")
+        if row:
+            return out if got.value else None
+        return bool(got.value)
+
+    def pending_samples(self) -> int:
+        v = ctypes.c_int64(0)
+        self._check(_lib.lib().rfa_pending_samples(self._h, ctypes.byref(v)), "rfa_pending_samples")
+        return v.value
+
+    def state_generation(self) -> int:
+        v = ctypes.c_int64(0)
+        self._check(_lib.lib().rfa_get_state_generation(self._h, ctypes.byref(v)), "rfa_get_state_generation")
+        return v.value
+
     def process_device(self, in_ptr: int, n_frames: int, frame_stride: int = 0, rows_ptr: int | None = None) -> None:
         """Device pointers (e.g. torch .data_ptr()); asynchronous on the engine stream."""
         self._check(_lib.lib().rfa_process(self._h, in_ptr, n_frames, frame_stride, rows_ptr), "rfa_process")

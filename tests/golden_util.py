@@ -130,6 +130,9 @@ def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> 
     return db_stats(got, exp, floor_db)["max_live"]
 
 
+FULL_ROW_LOG: list[dict] = []
+
+
 def full_row_diff(got: np.ndarray, exp: np.ndarray) -> float:
     """Max |dB difference| over EVERY bin (no floor); -inf must match -inf."""
     got = np.atleast_2d(np.asarray(got, np.float32))
@@ -137,4 +140,6 @@ def full_row_diff(got: np.ndarray, exp: np.ndarray) -> float:
     assert got.shape == exp.shape
     assert np.array_equal(np.isneginf(got), np.isneginf(exp)), "-inf bins differ"
     fin = np.isfinite(exp)
-    return float(np.max(np.abs(got[fin] - exp[fin])))
+    d = float(np.max(np.abs(got[fin] - exp[fin]))) if fin.any() else 0.0
+    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size)})
+    return d

@@ -99,7 +99,7 @@ def _analyzer(rfa, jenv, n, rows, frames, seed):
     assert h != 0
     data = np.frombuffer(signals.frames_bytes(n, frames, "s8", seed, tones=((0.13, 0.4), (0.31, 0.02)), noise=0.03),
                          np.int8).copy()
-    assert process(jenv.env, None, h, jenv.new_array(data), 0, 100_000_000, 2_000_000) == frames
+    assert process(jenv.env, None, h, jenv.new_array(data), 2 * n, 100_000_000, 2_000_000) == frames
     e = rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=rows)
     e.set_tuning(100_000_000, 2_000_000)
     e.process(data.tobytes(), frames, rows=False)
