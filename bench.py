@@ -18,8 +18,15 @@ Multi-GPU (no data-path collective):
   stream on its own GPU; weak scaling.
 * ``--mode shard`` (config 4): batches of 256 frames x 8192 points; each batch
   is split into contiguous frame ranges (sharding.frame_range), one per rank;
-  strong scaling (the batch is fixed as N grows).  ``--gather`` also gathers
-  the rows to rank 0 each call (the one real exchange of this mode).
+  strong scaling (the batch is fixed as N grows).  A call enqueues
+  ``--batches-per-call`` consecutive batches (rfa_process_batches: one kernel
+  launch) so small per-rank shards are not launch-bound.  ``--gather`` also
+  gathers the rows to rank 0 each call (the one real exchange of this mode).
+
+Companions on the same line (never ``value``), run by every rank in multi-GPU
+runs with per-rank times: ``f32`` (the headline on float32 IQ), ``config2``
+(16 K cf32 Hann), ``config4`` (the shard workload), ``config5`` (a 1 M-point
+stream per rank), ``demod`` and, on rank 0 of a 1-GPU run, ``cpu_baseline``.
 
 Launch: ``python bench.py --gpus N`` spawns N ranks itself (one process per
 GPU, started before anything touches the GPU, 127.0.0.1 rendezvous); under
@@ -67,10 +74,14 @@ def parse(argv=None):
     p.add_argument("--no-peak", action="store_true")
     p.add_argument("--ring-rows", type=int, default=500)
     p.add_argument("--gather", action="store_true", help="shard mode: gather every call's rows to rank 0")
+    p.add_argument("--batches-per-call", type=int, default=64,
+                   help="shard mode: batches per rfa_process_batches call (1 = one launch per batch)")
     p.add_argument("--pool-mib", type=int, default=768, help="input pool size (> Infinity Cache)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="cpu_baseline time budget (0 = skip)")
     p.add_argument("--f32-steps", type=int, default=4, help="steps of the float32-input companion run (0 = skip)")
     p.add_argument("--c5-steps", type=int, default=3, help="steps of the 1 M-point (config 5) companion (0 = skip)")
+    p.add_argument("--c2-steps", type=int, default=3, help="steps of the 16 K cf32 Hann (config 2) companion (0 = skip)")
+    p.add_argument("--c4-steps", type=int, default=3, help="steps of the 256 x 8192 shard (config 4) companion (0 = skip)")
     p.add_argument("--demod-steps", type=int, default=5,
                    help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
     p.add_argument("--profile-every", type=int, default=8,
@@ -83,7 +94,7 @@ def parse(argv=None):
     if a.frames == 0:
         a.frames = 500 if a.mode == "streams" else 256
     if a.calls_per_step == 0:
-        a.calls_per_step = 250 if a.mode == "streams" else 200
+        a.calls_per_step = 250 if a.mode == "streams" else max(1, 200 // max(1, a.batches_per_call))
     return a
 
 
@@ -243,32 +254,40 @@ def run_streams(args, ranks, fmt, steps, warmup, seed):
 
 
 def run_shard(args, ranks, steps, warmup):
-    """Config 4: every call is one batch of `frames` independent frames split over the
-    ranks (sharding.frame_range); rows stay on each rank's device unless --gather."""
+    """Config 4: every batch of `frames` independent frames is split over the ranks
+    (sharding.frame_range); a call enqueues `batches_per_call` consecutive batches of
+    this rank's frames (rfa_process_batches, one launch); rows stay on each rank's
+    device unless --gather.  Returns (slowest s, per-rank s, kernel ms, name, range, batches per call)."""
     import rfanalyzer_amd
     from rfanalyzer_amd import sharding
 
     torch = ranks.torch
     n, frames, fmt, calls = args.fft_size, args.frames, args.format, args.calls_per_step
+    kb = max(1, args.batches_per_call)
     s, e = sharding.frame_range(frames, ranks.rank, ranks.world)
     mine = e - s
     stream = torch.cuda.current_stream(ranks.device)
     eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, ring_rows=0, device=ranks.local)
     eng.set_stream(stream.cuda_stream)
-    # each rank holds its frame range of every pool batch (host-pinned slices in a
+    # this rank's frame range of every batch, packed batch after batch (host-pinned in a
     # deployment; device-resident here so the timed region measures the GPU path)
-    pool = [b.view(torch.uint8)[s * n * BPS[fmt]:e * n * BPS[fmt]].clone()
-            for b in make_pool(torch, n, frames, fmt, args.pool_mib, 4, ranks.device)]
-    rows = torch.empty(max(1, mine) * n, dtype=torch.float32, device=ranks.device)
+    bb = max(1, mine) * n * BPS[fmt]
+    src = make_pool(torch, n, frames, fmt, args.pool_mib, 4, ranks.device)
+    # at least the pool size of the other modes (past the Infinity Cache), a whole number of calls
+    count = max(len(src), -(-args.pool_mib * 2 ** 20 // bb))
+    count = -(-count // kb) * kb
+    pool = torch.empty(count * bb, dtype=torch.uint8, device=ranks.device)
+    for b in range(count):
+        pool[b * bb:b * bb + mine * n * BPS[fmt]].copy_(src[b % len(src)].view(torch.uint8)[s * n * BPS[fmt]:e * n * BPS[fmt]])
+    del src
+    rows = torch.empty(kb * max(1, mine) * n, dtype=torch.float32, device=ranks.device)
     gathered = None
     if args.gather and ranks.world > 1:
-        gathered = [torch.empty(((frames + ranks.world - 1) // ranks.world) * n, dtype=torch.float32,
+        gathered = [torch.empty(kb * ((frames + ranks.world - 1) // ranks.world) * n, dtype=torch.float32,
                                 device=ranks.device) for _ in range(ranks.world)]
         padded = torch.zeros_like(gathered[0])
     ctr = [0]
-
-    ptrs, rows_ptr = [b.data_ptr() for b in pool], rows.data_ptr()
-
+    base, rows_ptr = pool.data_ptr(), rows.data_ptr()
     every, sampling = max(1, args.profile_every), [False]
 
     def step(_k):
@@ -277,11 +296,12 @@ def run_shard(args, ranks, steps, warmup):
                 prof = sampling[0] and ctr[0] % every == 0
                 if prof:
                     eng.set_profiling(True)
-                eng.process_device(ptrs[ctr[0] % len(ptrs)], mine, 0, rows_ptr)
+                b0 = (ctr[0] * kb) % count
+                eng.process_batches(base + b0 * bb, kb, bb, mine, 0, rows_ptr)
                 if prof:
                     eng.set_profiling(False)
             if gathered is not None:
-                padded[:mine * n].copy_(rows[:mine * n])
+                padded[:kb * mine * n].copy_(rows[:kb * mine * n])
                 ranks.dist.all_gather(gathered, padded)
             ctr[0] += 1
 
@@ -294,7 +314,7 @@ def run_shard(args, ranks, steps, warmup):
     ms1, l1 = eng.kernel_time()
     name = eng.main_kernel_name()
     eng.close()
-    return slow, per, (ms1 - ms0) / max(1, l1 - l0), name, (s, e)
+    return slow, per, (ms1 - ms0) / max(1, l1 - l0), name, (s, e), kb
 
 
 # ----------------------------------------------------------------------------- companions
@@ -401,11 +421,42 @@ def _synthetic_frames(n, frames, fmt, seed=3):
     return iq.astype(np.float32)
 
 
-def cpu_baseline(args, n, seconds, threads=1):
-    """Reference loop (pffft + restated JVM loops, oracle/_ref) on host cores, bounded time."""
+def host_info():
+    """The host the CPU baseline ran on: model, online CPUs, the CPUs this process may
+    use (affinity) and the cgroup CPU quota, if any."""
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = os.cpu_count()
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+            info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def cpu_baseline(args, n, seconds):
+    """Reference loop (pffft + restated JVM loops, oracle/_ref) on host cores, bounded time:
+    one thread (the reference runs one FftProcessor thread) and then every CPU this
+    process may run on (os.sched_getaffinity), one independent loop per thread."""
     import numpy as np
 
     import oracle
+
+    hinfo = host_info()
+    # every CPU of the affinity mask, capped at 256 threads (the GPU boxes limit tasks per job)
+    threads = max(1, min(256, hinfo.get("affinity_cpus") or 1))
 
     fmt = {"s8": 0, "f32": 3}.get(args.format, 0)
     frames = max(1, (8 * 2 ** 20) // (n * 8))  # ~8 MB sample, processed repeatedly
@@ -414,7 +465,7 @@ def cpu_baseline(args, n, seconds, threads=1):
     ring_rows = 500
     fp = ctypes.POINTER(ctypes.c_float)
 
-    def run_ref(budget):
+    def run_ref(budget, ring_rows=ring_rows):
         """One thread = one reference FftProcessor loop (own ring + peaks)."""
         lib = oracle.ref()
         ring = np.full((ring_rows, n), -9999, np.float32)
@@ -442,21 +493,25 @@ def cpu_baseline(args, n, seconds, threads=1):
         what = "oracle C restatement (float64 FFT) -- reference pffft build absent"
     out = {"value": round(done * n / el / 1e6, 3), "unit": "Msamples/s", "cores": 1, "kind": kind,
            "sample": f"{frames} x {n}-pt {'s8' if fmt == 0 else 'f32'} frames looped for {el:.1f} s; {what}",
-           "lines_per_s": round(done / el, 2)}
+           "lines_per_s": round(done / el, 2), "host": hinfo}
     if kind == "reference" and threads > 1:
         # frame-parallel on the host's cores: one independent loop per thread;
         # ctypes releases the GIL for the duration of each ref_loop call
         import threading
 
+        # each thread writes its own 64-row ring (the per-frame ring copy is the same for any
+        # ring length; 500 rows x 64 K x 4 B per thread would not fit hundreds of threads)
         res = [None] * threads
-        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, run_ref(seconds / 2))) for i in range(threads)]
+        ths = [threading.Thread(target=lambda i=i: res.__setitem__(i, run_ref(seconds / 2, 64)))
+               for i in range(threads)]
         for t in ths:
             t.start()
         for t in ths:
             t.join()
         el = max(r[1] for r in res)
         out["multi_core"] = {"value": round(sum(r[0] for r in res) * n / el / 1e6, 3), "cores": threads,
-                             "sample": f"{threads} threads x the same loop for {el:.1f} s"}
+                             "sample": f"{threads} threads (every CPU in this process's affinity mask) x the "
+                                       f"same loop for {el:.1f} s"}
     return out
 
 
@@ -547,6 +602,7 @@ def main():
 
     n, frames, fmt, calls = args.fft_size, args.frames, args.format, args.calls_per_step
     result = {"metric": METRIC}
+    kb = 1
     if args.dry_run:
         slow, per = timed(ranks, lambda k: time.sleep(0.001 * (1 + ranks.rank)), args.steps, args.warmup)
         kernel_ms, kernel_name, span = 0.0, "dry-run", None
@@ -555,10 +611,11 @@ def main():
         slow, per, kernel_ms, kernel_name = run_streams(args, ranks, fmt, args.steps, args.warmup, 3 + ranks.rank)
         mine = frames
     else:
-        slow, per, kernel_ms, kernel_name, span = run_shard(args, ranks, args.steps, args.warmup)
-        mine = span[1] - span[0]
+        slow, per, kernel_ms, kernel_name, span, kb = run_shard(args, ranks, args.steps, args.warmup)
+        mine = (span[1] - span[0]) * kb
 
-    total_frames = (ranks.world if args.mode == "streams" else 1) * frames * calls * args.steps
+    batches = kb if args.mode == "shard" else 1
+    total_frames = (ranks.world if args.mode == "streams" else 1) * frames * batches * calls * args.steps
     samples = total_frames * n
     msps = samples / slow / 1e6
     s_in = BPS[fmt]
@@ -585,12 +642,15 @@ def main():
                     f"ring {args.ring_rows} rows, one stream per GPU")
     else:
         workload = (f"config4: batches of {frames} frames x {n}-pt FFT, {args.window}, {fmt} IQ, frames sharded "
-                    f"over {ranks.world} GPU(s) (contiguous ranges){', rows gathered to rank 0' if args.gather else ''}")
-    result["config"] = {"workload": workload, "fft_size": n, "frames_per_call": frames, "calls_per_step": calls,
-                        "input_format": fmt, "parallelism": f"{args.mode}{ranks.world}"}
+                    f"over {ranks.world} GPU(s) (contiguous ranges), {kb} batches per rfa_process_batches call"
+                    f"{', rows gathered to rank 0' if args.gather else ''}")
+    result["config"] = {"workload": workload, "fft_size": n, "frames_per_call": frames * batches,
+                        "calls_per_step": calls, "input_format": fmt, "parallelism": f"{args.mode}{ranks.world}"}
     if args.mode == "streams":
         result["config"].update({"avg": args.avg, "ema_alpha": args.ema_alpha, "peak_hold": not args.no_peak,
                                  "ring_rows": args.ring_rows})
+    else:
+        result["config"]["frames_per_batch"] = frames
     result["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                           "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                           "kernel": kernel_name, "kernel_ms": round(kernel_ms, 4),
@@ -599,12 +659,13 @@ def main():
                                     "main-kernel launch of the timed region"}
     single = ranks.rank == 0 and ranks.world == 1 and not args.dry_run
     if single:
-        tr, src = pmc_traffic(args, fmt, n, frames)
+        tr, src = pmc_traffic(args, fmt, n, mine)
         result["roofline"]["traffic"] = tr
         result["roofline"]["traffic_source"] = src
-        va = sq_valu(args, fmt, n, frames)
+        va = sq_valu(args, fmt, n, mine)
         if va is not None:
             result["roofline"]["valu"] = va
+    if ranks.rank == 0 and not args.dry_run:
         gbps, ok = copy_ceiling(torch, ranks.device)
         result["roofline"]["copy_GBps"] = gbps
         result["roofline"]["copy_kernel"] = "rfa_stream_copy (librfa float4 copy)" + ("" if ok else " MISMATCH")
@@ -613,42 +674,94 @@ def main():
             # step level: every byte the step must move (raw in, ring row out, EMA + peak read+write) / step time
             step_bytes = frames * n * (s_in + 4) + 16 * n
             result["roofline"]["step_frac"] = round(step_bytes * calls * args.steps / slow / 1e9 / HBM_PEAK_GBPS, 4)
-    if single and args.mode == "streams" and fmt != "f32" and args.f32_steps > 0:
-        # BASELINE.json asks for 8-bit AND float32 IQ: the same workload on complex-float32
-        # input (12 B/sample algorithmic), reported beside the headline (never `value`)
-        el32, _, k32, _ = run_streams(args, ranks, "f32", args.f32_steps, 1, 103)
-        alg32 = frames * n * (BPS["f32"] + 4)
-        result["f32"] = {"value": round(args.f32_steps * calls * frames * n / el32 / 1e6, 2), "unit": "Msamples/s",
-                         "ms_per_step": round(el32 * 1e3 / args.f32_steps, 4), "kernel_ms": round(k32, 4),
-                         "roofline_achieved_GBps": round(alg32 / (k32 * 1e-3) / 1e9, 1),
-                         "roofline_frac": round(alg32 / (k32 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                         "alg_bytes_per_launch": alg32}
-    if single and args.mode == "streams" and n != (1 << 20) and args.c5_steps > 0:
-        # config 5's per-GPU stream: 1 M-point FFT, same stateful settings, reported beside
-        # the headline (never `value`); its main-kernel time spans the large-N pair
-        import copy
-        a5 = copy.copy(args)
-        a5.fft_size, a5.frames, a5.calls_per_step = 1 << 20, 16, 30
-        el5, _, k5, name5 = run_streams(a5, ranks, fmt, args.c5_steps, 1, 203)
-        alg5 = a5.frames * a5.fft_size * (s_in + 4)
-        result["config5"] = {"workload": f"config5 per GPU: 1048576-pt FFT, {args.window}, {fmt} IQ, "
-                                         f"{'EMA' if args.avg == 'ema' else args.avg} + peak-hold, ring "
-                                         f"{args.ring_rows} rows, 16 frames per call",
-                             "value": round(args.c5_steps * a5.calls_per_step * a5.frames * a5.fft_size / el5 / 1e6, 2),
-                             "unit": "Msamples/s", "ms_per_step": round(el5 * 1e3 / args.c5_steps, 4),
-                             "kernel_ms": round(k5, 4), "kernel": name5,
-                             "roofline_achieved_GBps": round(alg5 / (k5 * 1e-3) / 1e9, 1),
-                             "roofline_frac": round(alg5 / (k5 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                             "alg_bytes_per_launch": alg5,
-                             "note": "kernel_ms = the whole large-N launch (front kernel + 32 K kernel B)"}
-    if single and args.demod_steps > 0:
-        result["demod"] = demod_companion(torch, ranks.device, args.demod_steps)
+    if args.mode == "streams":
+        companions(args, ranks, result)
     if ranks.rank == 0 and ranks.world == 1 and args.cpu_seconds > 0 and args.mode == "streams":
-        result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds, min(16, os.cpu_count() or 1))
+        result["cpu_baseline"] = cpu_baseline(args, n, args.cpu_seconds)
         result["cpu_baseline"]["config1"] = config1_replay(not args.dry_run)
     if ranks.rank == 0:
         print(json.dumps(result), flush=True)
     ranks.close()
+
+
+def _stream_companion(args, ranks, steps, seed, **over):
+    """One run_streams workload with some settings replaced; every rank takes part."""
+    import copy
+    a = copy.copy(args)
+    for k, v in over.items():
+        setattr(a, k, v)
+    fmt = over.get("format", args.format)
+    if args.dry_run:
+        slow, per = timed(ranks, lambda k: time.sleep(0.0005 * (1 + ranks.rank)), steps, 1)
+        return a, slow, per, 0.0, "dry-run"
+    slow, per, k, name = run_streams(a, ranks, fmt, steps, 1, seed)
+    return a, slow, per, k, name
+
+
+def _roof(alg, k_ms):
+    gbps = alg / (k_ms * 1e-3) / 1e9 if k_ms > 0 else 0.0
+    return {"roofline_achieved_GBps": round(gbps, 1), "roofline_frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "alg_bytes_per_launch": alg}
+
+
+def companions(args, ranks, result):
+    """Other BASELINE configs beside the headline (never `value`).  In multi-GPU runs every
+    rank runs them (streams: one per rank, weak; config 4: the batch split, strong) and the
+    per-rank seconds are reported; values are whole-job Msamples/s."""
+    W = ranks.world
+    fmt, n = args.format, args.fft_size
+    if fmt != "f32" and args.f32_steps > 0:
+        # BASELINE.json asks for 8-bit AND float32 IQ: the headline workload on complex-float32
+        # input (12 B/sample algorithmic)
+        a, el, per, k, _ = _stream_companion(args, ranks, args.f32_steps, 103 + ranks.rank, format="f32")
+        result["f32"] = {"value": round(W * args.f32_steps * a.calls_per_step * a.frames * n / el / 1e6, 2),
+                         "unit": "Msamples/s", "ms_per_step": round(el * 1e3 / args.f32_steps, 4),
+                         "kernel_ms": round(k, 4), "per_rank_s": [round(x, 6) for x in per],
+                         **_roof(a.frames * n * (BPS["f32"] + 4), k)}
+    if args.c2_steps > 0:
+        # config 2: synthetic 20 Msps complex-float32 IQ, 16384-pt Hann, waterfall ring, no averaging
+        a, el, per, k, name = _stream_companion(args, ranks, args.c2_steps, 303 + ranks.rank, format="f32",
+                                                fft_size=16384, window="hann", frames=4096, calls_per_step=30,
+                                                avg="none", no_peak=True)
+        result["config2"] = {"workload": "config2 per GPU: 16384-pt Hann FFT, cf32 IQ (20 Msps), ring 500 rows, "
+                                         "4096 frames per call, no averaging",
+                             "value": round(W * args.c2_steps * a.calls_per_step * a.frames * a.fft_size / el / 1e6, 2),
+                             "unit": "Msamples/s", "ms_per_step": round(el * 1e3 / args.c2_steps, 4),
+                             "kernel_ms": round(k, 4), "kernel": name, "per_rank_s": [round(x, 6) for x in per],
+                             **_roof(a.frames * a.fft_size * (BPS["f32"] + 4), k)}
+    if args.c4_steps > 0:
+        import copy
+        a4 = copy.copy(args)
+        a4.mode, a4.fft_size, a4.frames, a4.format = "shard", 8192, 256, fmt if fmt in ("s8", "u8") else "s8"
+        a4.calls_per_step, a4.batches_per_call, a4.gather = 10, 64, False
+        if args.dry_run:
+            el, per = timed(ranks, lambda k: time.sleep(0.0005 * (1 + ranks.rank)), args.c4_steps, 1)
+            k4, name4, mine = 0.0, "dry-run", 256 // W
+        else:
+            el, per, k4, name4, span, _ = run_shard(a4, ranks, args.c4_steps, 1)
+            mine = span[1] - span[0]
+        total = args.c4_steps * a4.calls_per_step * a4.batches_per_call * a4.frames * a4.fft_size
+        nb = args.c4_steps * a4.calls_per_step * a4.batches_per_call
+        result["config4"] = {"workload": f"config4: batches of 256 x 8192-pt {a4.format} frames sharded over {W} "
+                                         f"GPU(s), {a4.batches_per_call} batches per rfa_process_batches call",
+                             "value": round(total / el / 1e6, 2), "unit": "Msamples/s", "scaling": "strong",
+                             "us_per_batch": round(el / nb * 1e6, 3), "kernel_ms": round(k4, 4), "kernel": name4,
+                             "per_rank_s": [round(x, 6) for x in per],
+                             **_roof(a4.batches_per_call * mine * a4.fft_size * (BPS[a4.format] + 4), k4)}
+    if n != (1 << 20) and args.c5_steps > 0:
+        # config 5: one independent 1 M-point stream per GPU, same stateful settings
+        a, el, per, k, name = _stream_companion(args, ranks, args.c5_steps, 203 + ranks.rank, fft_size=1 << 20,
+                                                frames=16, calls_per_step=30)
+        result["config5"] = {"workload": f"config5 per GPU: 1048576-pt FFT, {args.window}, {fmt} IQ, "
+                                         f"{'EMA' if args.avg == 'ema' else args.avg} + peak-hold, ring "
+                                         f"{args.ring_rows} rows, 16 frames per call, one stream per GPU",
+                             "value": round(W * args.c5_steps * a.calls_per_step * a.frames * a.fft_size / el / 1e6, 2),
+                             "unit": "Msamples/s", "scaling": "weak", "ms_per_step": round(el * 1e3 / args.c5_steps, 4),
+                             "kernel_ms": round(k, 4), "kernel": name, "per_rank_s": [round(x, 6) for x in per],
+                             **_roof(a.frames * a.fft_size * (BPS[fmt] + 4), k),
+                             "note": "kernel_ms = the whole large-N launch (front kernel + 32 K kernel B)"}
+    if ranks.rank == 0 and args.demod_steps > 0 and not args.dry_run:
+        result["demod"] = demod_companion(ranks.torch, ranks.device, args.demod_steps)
 
 
 if __name__ == "__main__":

@@ -133,6 +133,18 @@ RFA_API int rfa_synchronize(rfa_handle *h);
 RFA_API int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 RFA_API int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 
+/* Multi-batch enqueue: exactly n_batches consecutive rfa_process calls (ring,
+ * peaks, EMA and channel means advance batch after batch), batch b reading
+ * frames_per_batch frames at in + b * batch_stride_bytes + f * frame_stride_bytes
+ * and writing its rows (if rows != NULL) at rows + b * frames_per_batch * N.
+ * When the batches are packed (batch_stride_bytes == frames_per_batch * frame
+ * stride) the whole run is ONE kernel launch, so small batches (BASELINE
+ * config 4: 256 x 8192 points) stop paying a host call + launch each.
+ * Device pointers, asynchronous on the handle stream; channel means are those
+ * of the last batch. */
+RFA_API int rfa_process_batches(rfa_handle *h, const void *in, size_t n_batches, size_t batch_stride_bytes,
+                                size_t frames_per_batch, size_t frame_stride_bytes, float *rows);
+
 /* Scheduler.run's FFT branch, one raw packet at a time (Scheduler.kt:252-273
  * with the converters' fillPacketIntoSamplePacket, Signed8BitIQConverter.java:80-98,
  * Unsigned8BitIQConverter.java:80-98, Signed16BitIQConverter.kt:89-124): the

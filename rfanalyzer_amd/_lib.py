@@ -92,6 +92,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_synchronize": (ctypes.c_int, [_h]),
         "rfa_process": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_process_host": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
+        "rfa_process_batches": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                               ctypes.c_size_t, _vp]),
         "rfa_set_tuning": (ctypes.c_int, [_h, ctypes.c_int64, ctypes.c_int64]),
         "rfa_push_packet": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64, _vp,
                                            ctypes.POINTER(ctypes.c_int32)]),

@@ -42,20 +42,15 @@ struct rfa_handle {
     float *d_dit_db = nullptr;        // caller rows of a batch, residue-major, before cols_to_rows
     size_t d_dit_db_cap = 0;
     int dit_frames = 1;               // frames per kernel-A/B pair (scratch <= kDitScratch)
-    int dif_pipe = 6;                 // RFA_DIF_PIPE: frame groups of the pipelined front kernel (8-bit input; 0 off)
-    int variant = 0;                  // RFA_KERNEL=narrow selects the narrow kernel (comparison)
-    int persist = 0;                  // RFA_PERSIST: wide-kernel persistent workgroups per CU
-    long long stagger_ns = 0;         // RFA_STAGGER_NS
-    int stage = 1;                    // RFA_STAGE: LDS-DMA staged input in the wide kernel
-    unsigned *d_queue = nullptr;      // staged kernels' work-queue counters (RFA_DQ=1; default static items)
-    std::string stamps_file;          // RFA_STAMPS_FILE (profiling only): phase stamps appended per launch
+    int dif_pipe = 6;                 // frame groups of the pipelined front kernel (8-bit input)
+    int variant = 0;                  // 1: the narrow kernel (A/B builds: RFA_KERNEL=narrow)
+    int stage = 1;                    // LDS-DMA staged input in the wide kernel (A/B builds: RFA_STAGE=0 off)
+    // profiling / ablation hooks, set only by A/B builds (-DRFA_AB_BUILD, scripts/build_variant.sh);
+    // the product library reads no environment and never takes these paths
+    std::string stamps_file;          // RFA_STAMPS_FILE: phase stamps appended per launch
     unsigned long long *d_stamps = nullptr;
-    int diag = 0;                     // RFA_DIAG ablation variant (profiling only)
-    int max_logm = 14;                // RFA_MAX_LOGM experiment switch
-    int wide_big = 15;                // RFA_WIDE_LOGM: 15 (32 K workgroups) or 14 for N > 16 K
+    int diag = 0;                     // RFA_DIAG ablation variant
     int ring_logrs = 0;               // ring row order (fft_kernels.h ring_pos): residue split of the main kernel
-    int w64 = 0;                      // RFA_W64=1: the four-step wave kernel at N = 64 K (opt-in)
-    int prio = 0;                     // RFA_W64_PRIO (speed only)
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
     float *d_ring = nullptr, *d_ring_tmp = nullptr;
@@ -67,15 +62,7 @@ struct rfa_handle {
     float *d_ema = nullptr;
     float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
     int state_chunks = 1;
-    int state_fused = 1;              // RFA_STATE_FUSED=0: two-kernel chunked scan
-    // RFA_STATE_OVERLAP=P: a ring-resident batch runs as P frame parts; the peak /
-    // EMA update of part p runs on state_stream beside the FFT of part p + 1
-    int state_overlap = 0;
-    bool state_lazy = false;          // RFA_STATE_JOIN=lazy: join state_stream at the next entry point
-    hipStream_t state_stream = nullptr;
-    hipEvent_t ev_fft = nullptr, ev_state[2] = {nullptr, nullptr};
-    long long part_seq = 0;           // frame parts launched so far (ev_state slot = seq & 1)
-    bool state_pending = false;       // state_stream work not yet joined into stream
+    int state_fused = 1;              // single-launch chunked scan (A/B builds: RFA_STATE_FUSED=0 two kernels)
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -196,24 +183,10 @@ int ensure_pinned(rfa_handle *h, size_t bytes) {
     return RFA_OK;
 }
 
-// Order the handle stream after the state-stream work of overlapped batches.
-int join_state(rfa_handle *h) {
-    if (!h->state_pending) return RFA_OK;
-    h->state_pending = false;
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_state[(h->part_seq - 1) & 1], 0));
-    return RFA_OK;
-}
-
-int set_device_nojoin(rfa_handle *h) {
+int set_device(rfa_handle *h) {
     hipError_t e = hipSetDevice(h->device);
     if (e != hipSuccess) return hip_fail(h, e, "hipSetDevice");
     return RFA_OK;
-}
-
-// Every entry point but rfa_process starts here: pending state work is joined first.
-int set_device(rfa_handle *h) {
-    int rc = set_device_nojoin(h);
-    return rc ? rc : join_state(h);
 }
 
 // Collect finished profiling event pairs.
@@ -286,7 +259,6 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         B.complex_out = a.complex_out ? a.complex_out + (size_t)f0 * n : nullptr;
         B.ring_base = a.ring_base - f0;  // frame f0 + f of the call is frame f of this pair
         B.ring_first = a.ring_first - f0;
-        B.persist = 0;
         B.stage = 0;
         B.diag = 0;
         B.stamps = nullptr;
@@ -307,17 +279,11 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_fine = h->d_twf;
     a.tw_shift = h->tw_shift;
     a.diag = h->diag;
-    a.persist = h->persist;
-    a.stagger_ns = h->stagger_ns;
     a.stage = h->stage;
-    a.queue = h->d_queue;
     if (h->d_stamps) {
         a.diag = 32;
         a.stamps = h->d_stamps;
     }
-    a.wide_big = h->wide_big;
-    a.w64 = h->w64;
-    a.prio = h->prio;
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
     if (a.window == h->d_window) a.window_il = h->d_window_il;
@@ -325,7 +291,6 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     // the ring order is a property of the wide kernel's residue split (ring_pos)
     if (a.ring && h->ring_logrs && a.variant == 1 && h->logn <= 17)
         return fail(h, RFA_ERR_INVALID, "ring order needs the wide kernel");
-    a.max_logm = h->max_logm;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (h->profile) {
         // collect finished pairs without blocking; block (oldest first) only when far behind
@@ -474,8 +439,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMalloc(tabs[i], n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(*tabs[i], src[i], n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
     }
-    if (const char *d = std::getenv("RFA_WIDE_LOGM")) h->wide_big = std::atoi(d) == 14 ? 14 : 15;
-    const int m_sub = 1 << rfa::wide_logm(logn, h->wide_big);
+    const int m_sub = 1 << rfa::wide_logm(logn);
     if (n > m_sub && logn <= 17) {  // interleaved copy for the wide kernel's decimation-in-frequency pre-stage
         const int rs = n / m_sub;
         std::vector<float> il(n);
@@ -497,51 +461,30 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
             if (hipMemcpy(*u.dst, u.src, u.bytes, hipMemcpyHostToDevice) != hipSuccess) return bail(RFA_ERR_HIP);
         }
         // scratch per kernel pair <= 128 MB so it stays in the 256 MB Infinity Cache
-        size_t mb = 128;
-        if (const char *d = std::getenv("RFA_DIT_SCRATCH_MB")) mb = (size_t)std::max(8, std::atoi(d));  // A/B only
+        const size_t mb = 128;
         h->dit_frames = (int)std::max<size_t>(1, (mb << 20) / ((size_t)n * sizeof(float2)));
     }
     if (rfa::wide_supported(logn)) {
-        std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn, h->wide_big));
+        std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn));
         if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_wide_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
     }
+#ifdef RFA_AB_BUILD
+    // A/B and profiling builds only (scripts/build_variant.sh): ablation switches
     if (const char *d = std::getenv("RFA_KERNEL")) h->variant = std::string(d) == "narrow" ? 1 : 0;
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
-    if (const char *d = std::getenv("RFA_PERSIST")) h->persist = std::atoi(d);
     if (const char *d = std::getenv("RFA_DIF_PIPE")) h->dif_pipe = std::max(0, std::atoi(d));
-    if (const char *d = std::getenv("RFA_STAGGER_NS")) h->stagger_ns = std::atoll(d);
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
-    {
-        // dynamic work queue for the staged one-residue kernels: off by default (it
-        // measured slower than the static stride with the current code)
-        const char *d = std::getenv("RFA_DQ");
-        if (d && std::atoi(d) != 0) {
-            if (hipMalloc(&h->d_queue, 16 * sizeof(unsigned)) != hipSuccess) return bail(RFA_ERR_NOMEM);
-            if (hipMemset(h->d_queue, 0, 16 * sizeof(unsigned)) != hipSuccess) return bail(RFA_ERR_HIP);
-        }
-    }
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
         h->stamps_file = d;
         if (hipMalloc(&h->d_stamps, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemset(h->d_stamps, 0, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_HIP);
     }
-    if (const char *d = std::getenv("RFA_MAX_LOGM")) h->max_logm = std::atoi(d);
-    // ring row order: residue-major when the wide kernel splits N into residue
-    // sub-FFTs (whole-line stores per workgroup); RFA_RING_NATURAL=1 keeps natural order
-    if (const char *d = std::getenv("RFA_W64")) h->w64 = std::atoi(d) != 0;
-    if (const char *d = std::getenv("RFA_W64_PRIO")) h->prio = std::atoi(d);
-    if (h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(logn) && logn <= 17) {
-        const char *nat = std::getenv("RFA_RING_NATURAL");
-        if (nat && std::atoi(nat) != 0) h->w64 = 0;  // the wave kernel only writes its own order
-        else h->ring_logrs = rfa::ring_logrs_for(logn, h->wide_big, h->w64);
-    } else {
-        h->w64 = 0;
-        const char *nat = std::getenv("RFA_RING_NATURAL");
-        if (logn > 17 && !(nat && std::atoi(nat) != 0))  // large-N kernel B: ring block s holds bins S q + s
-            h->ring_logrs = rfa::ring_logrs_for(logn, h->wide_big, 0);
-    }
+#endif
+    // ring row order: residue-major when the main kernel splits N into residue
+    // sub-FFTs (whole-line stores per workgroup), natural otherwise
+    if (h->variant != 1 || logn > 17) h->ring_logrs = rfa::ring_logrs_for(logn);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
     h->tw_shift = (logn + 1) / 2;
@@ -571,26 +514,13 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (h->d_peaks || h->d_ema) {
         // enough (bin, chunk) threads to fill the chip (~2^19) for large batches
         h->state_chunks = (int)std::min<size_t>(32, std::max<size_t>(1, ((size_t)1 << 20) / n));
+#ifdef RFA_AB_BUILD
         if (const char *d = std::getenv("RFA_STATE_CHUNKS")) h->state_chunks = std::max(1, std::min(64, std::atoi(d)));
         if (const char *d = std::getenv("RFA_STATE_FUSED")) h->state_fused = std::atoi(d);
+#endif
         if (h->state_chunks > 1 &&
             hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
             return bail(RFA_ERR_NOMEM);
-        if (const char *d = std::getenv("RFA_STATE_OVERLAP")) h->state_overlap = std::max(0, std::min(16, std::atoi(d)));
-        if (const char *d = std::getenv("RFA_STATE_JOIN")) h->state_lazy = std::string(d) == "lazy";
-        if (h->state_overlap >= 2 && h->d_ring) {
-            // RFA_STATE_PRIO=1: the state stream at the lowest priority, so the dispatcher
-            // prefers the FFT's whole-CU workgroups when a CU frees up
-            int lo = 0, hi = 0;
-            const char *pr = std::getenv("RFA_STATE_PRIO");
-            if (pr && std::atoi(pr) && hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
-            if (hipStreamCreateWithPriority(&h->state_stream, hipStreamNonBlocking, pr && std::atoi(pr) ? lo : 0) !=
-                    hipSuccess ||
-                hipEventCreateWithFlags(&h->ev_fft, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&h->ev_state[0], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&h->ev_state[1], hipEventDisableTiming) != hipSuccess)
-                return bail(RFA_ERR_HIP);
-        }
     }
     if (hipMalloc(&h->d_boxcar, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (clear_ring(h) || reset_peaks_ema(h)) return bail(RFA_ERR_HIP);
@@ -603,16 +533,9 @@ int rfa_destroy(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->state_stream) {
-        hipStreamSynchronize(h->state_stream);
-        hipStreamDestroy(h->state_stream);
-    }
-    for (hipEvent_t e : {h->ev_fft, h->ev_state[0], h->ev_state[1]})
-        if (e) hipEventDestroy(e);
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     hipFree(h->d_stamps);
-    hipFree(h->d_queue);
     hipFree(h->d_window);
     hipFree(h->d_window_none);
     hipFree(h->d_window_black);
@@ -651,7 +574,7 @@ const char *rfa_last_error(const rfa_handle *h) { return h ? h->err.c_str() : "n
 
 int rfa_set_stream(rfa_handle *h, void *stream) {
     if (!h) return RFA_ERR_INVALID;
-    if (int rc = set_device(h)) return rc;  // pending state work joins the old stream
+    if (int rc = set_device(h)) return rc;
     h->stream = (hipStream_t)stream;
     return RFA_OK;
 }
@@ -721,8 +644,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     if (n_frames > (size_t)0x7fffffff) return fail(h, RFA_ERR_INVALID, "too many frames");
     if (n_frames == 0) return RFA_OK;
     if (h->pending_ring_rows >= 0) {
-        int rc = join_state(h);  // the resize reads the ring on the handle stream
-        if (!rc) rc = apply_ring_resize(h);
+        int rc = apply_ring_resize(h);
         if (rc) return rc;
     }
     const bool need_state = h->d_peaks || h->d_ema;
@@ -769,61 +691,9 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
         a.ring_logrs = h->ring_logrs;
     }
-    // Overlapped form (RFA_STATE_OVERLAP=P): the batch runs as P frame parts of at
-    // most R/2 frames; part p's peak / EMA update runs on state_stream while the FFT
-    // of part p + 1 runs on the handle stream.  The FFT of part q only has to wait
-    // for the state update of part q - 2: parts q - 1 and q together hold at most R
-    // frames, so part q never overwrites a ring row that part q - 1's update reads.
-    const int n_parts = h->state_overlap;
-    const int part_len = n_parts >= 2 ? (int)((n_frames + n_parts - 1) / n_parts) : 0;
-    const bool overlap = rows_in_ring && need_state && !need_chan && h->state_stream && n_parts >= 2 &&
-                         part_len >= 32 && 2 * part_len <= h->ring_rows;
-    if (overlap) {
-        const long long R = h->ring_rows;
-        for (int f0 = 0; f0 < (int)n_frames; f0 += part_len) {
-            const int cnt = std::min<int>(part_len, (int)n_frames - f0);
-            const int base = (int)((((long long)h->write_index - f0) % R + R) % R);
-            const long long q = h->part_seq;
-            if (q >= 2) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_state[q & 1], 0));
-            FftLaunch p = a;
-            p.in = a.in + (size_t)f0 * stride;
-            p.n_frames = cnt;
-            p.ring_base = base;
-            p.ring_first = 0;
-            int rc = launch_main(h, p);
-            if (rc) return rc;
-            HIPCHK(h, hipEventRecord(h->ev_fft, h->stream));
-            HIPCHK(h, hipStreamWaitEvent(h->state_stream, h->ev_fft, 0));
-            rfa::StateLaunch s;
-            s.n = n;
-            s.n_frames = cnt;
-            s.peaks = h->d_peaks;
-            s.ema = h->d_ema;
-            s.ema_alpha = h->cfg.ema_alpha;
-            s.part = h->d_state_part;
-            s.max_chunks = h->state_chunks;
-            s.fused = h->state_fused;
-            s.stream = h->state_stream;
-            s.rows = h->d_ring;
-            s.ring_rows = h->ring_rows;
-            s.ring_base = base;
-            s.ring_logrs = h->ring_logrs;
-            HIPCHK(h, rfa::launch_state(s));
-            HIPCHK(h, hipEventRecord(h->ev_state[q & 1], h->state_stream));
-            h->part_seq = q + 1;
-            h->state_pending = true;
-        }
-        if (!h->state_lazy) {
-            int rc = join_state(h);
-            if (rc) return rc;
-        }
-    } else {
-        int rc = join_state(h);  // a lazy overlapped batch before this one
-        if (rc) return rc;
-        rc = launch_main(h, a);
-        if (rc) return rc;
-    }
-    if ((need_state || need_chan) && !overlap) {
+    int rc = launch_main(h, a);
+    if (rc) return rc;
+    if (need_state || need_chan) {
         rfa::StateLaunch s;
         s.n = n;
         s.n_frames = (int)n_frames;
@@ -867,9 +737,31 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
 
 int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows) {
     if (!h || (!in && n_frames)) return RFA_ERR_INVALID;
-    int rc = set_device_nojoin(h);  // process_impl joins (or overlaps) itself
+    int rc = set_device(h);
     if (rc) return rc;
     return process_impl(h, in, n_frames, frame_stride_bytes, rows, h->d_window, h->cfg.input_format);
+}
+
+int rfa_process_batches(rfa_handle *h, const void *in, size_t n_batches, size_t batch_stride_bytes,
+                        size_t frames_per_batch, size_t frame_stride_bytes, float *rows) {
+    if (!h || (!in && n_batches && frames_per_batch)) return RFA_ERR_INVALID;
+    if (n_batches == 0 || frames_per_batch == 0) return RFA_OK;
+    int rc = set_device(h);
+    if (rc) return rc;
+    const size_t stride = frame_stride_bytes ? frame_stride_bytes : (size_t)h->n * bytes_per_sample(h->cfg.input_format);
+    if (n_batches == 1 || batch_stride_bytes == frames_per_batch * stride) {
+        // packed: one batch of n_batches * frames_per_batch frames is the same frame stream
+        // (the ring and the peak / EMA recursion see the frames in the same order)
+        if (n_batches > (size_t)0x7fffffff / frames_per_batch) return fail(h, RFA_ERR_INVALID, "too many frames");
+        return process_impl(h, in, n_batches * frames_per_batch, stride, rows, h->d_window, h->cfg.input_format);
+    }
+    for (size_t b = 0; b < n_batches; b++) {
+        rc = process_impl(h, static_cast<const uint8_t *>(in) + b * batch_stride_bytes, frames_per_batch, stride,
+                          rows ? rows + b * frames_per_batch * (size_t)h->n : nullptr, h->d_window,
+                          h->cfg.input_format);
+        if (rc) return rc;
+    }
+    return RFA_OK;
 }
 
 int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows) {
@@ -893,8 +785,6 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
     if (rc) return rc;
     if (rows)
         HIPCHK(h, hipMemcpyAsync(rows, d_rows, n_frames * (size_t)h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
-    rc = join_state(h);
-    if (rc) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
 }
@@ -1320,8 +1210,7 @@ int rfa_set_profiling(rfa_handle *h, int enable) {
 const char *rfa_main_kernel_name(const rfa_handle *h) {
     if (!h) return "";
     if (h->logn > 17) return "dif_front_kernel+fft_wide_kernel";  // the large-N pair (fft_large.hip)
-    if (h->w64 && h->logn == 16) return "fft_w64_kernel";
-    const bool wide = h->variant != 1 && h->max_logm == 14 && rfa::wide_supported(h->logn);
+    const bool wide = h->variant != 1 && rfa::wide_supported(h->logn);
     return wide ? "fft_wide_kernel" : "fft_rows_kernel";
 }
 

@@ -59,18 +59,11 @@ struct FftLaunch {
     // in + (u * M) complex, outputs bins S q + s of an N = S * M frame; its dB rows
     // target is residue-major (block s), like the ring
     int dif_ss = 0;
-    int wide_big = 15;        // wide_logm() for N > 16 K (RFA_WIDE_LOGM)
-    int persist = 0;          // wide kernel: >0 = persistent grid of persist workgroups per CU
-    long long stagger_ns = 0; // wide kernel, persistent: start delay of the second half of the grid
-    int stage = 1;            // wide kernel: LDS-DMA staged 8/16-bit input when aligned (RFA_STAGE=0 disables)
-    int w64 = 0;              // N = 64 K: the four-step "wave" kernel (RFA_W64=1, opt-in; ring_logrs 6)
-    int prio = 0;             // w64 kernel: s_setprio 1 for waves with (wave & prio) != 0 (RFA_W64_PRIO, speed only)
-    // staged one-residue kernels: work-queue counter [0] + finisher count [1], zero at
-    // launch and zeroed again by the kernel's last workgroup (null = static item stride)
-    unsigned *queue = nullptr;
-    int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only
-    int max_logm = 14;  // largest sub-FFT per workgroup (13 = experiment: 2 workgroups per CU)
-    int diag = 0;  // ablation variant (profiling only): 1 no loads, 2 no stores, 4 no FFT passes, 32 stamps
+    int stage = 1;      // wide kernel: LDS-DMA staged 8/16-bit input when aligned (0 only in A/B builds)
+    int variant = 0;    // 0 auto (wide kernel for N = 2^13..2^17), 1 narrow kernel only (seam windows)
+    // A/B builds only (RFA_AB_BUILD): ablation variant (1 no loads, 2 no stores, 4 no FFT
+    // passes, 32 phase stamps); always 0 in the product library
+    int diag = 0;
     unsigned long long *stamps = nullptr;  // diag 32: [blocks][16][8] s_memrealtime phase stamps
     hipStream_t stream = nullptr;
 };
@@ -81,11 +74,11 @@ hipError_t launch_fft(const FftLaunch &a);
 // M = 8 K / 16 K / 32 K) for N = 2^13..2^17, and kernel B of the large-N pair.
 bool wide_supported(int logn);
 // ring order (ring_pos logrs) the main kernel writes for N = 2^logn
-int ring_logrs_for(int logn, int wide_big, int w64);
+int ring_logrs_for(int logn);
 constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
-// sub-FFT size of the wide kernel: N itself up to 16 K, else 2^big (15: one
-// 32 K-point workgroup per CU; 14: 16 K, two per CU) with N / 2^big residues
-inline int wide_logm(int logn, int big) { return logn <= 14 ? logn : big; }
+// sub-FFT size of the wide kernel: N itself up to 16 K, else 32 K (one
+// 32 K-point workgroup per CU) with N / 32 K residues
+inline int wide_logm(int logn) { return logn <= 14 ? logn : 15; }
 std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
 

@@ -325,6 +325,7 @@ static hipError_t launch_one(const FftLaunch &a) {
 template <int LOGM, int RS, bool CO>
 static hipError_t by_fmt(const FftLaunch &a) {
     if constexpr (!CO) {
+#ifdef RFA_AB_BUILD
         if (a.diag) {  // ablation builds (profiling only): 16K/64K, s8 and f32
             if constexpr (LOGM == 14 && (RS == 1 || RS == 4)) {
 #define RFA_DIAG(D)                                                   \
@@ -338,6 +339,7 @@ static hipError_t by_fmt(const FftLaunch &a) {
             }
             return hipErrorInvalidValue;
         }
+#endif
     }
     switch (a.fmt) {
     case 0: return launch_one<LOGM, RS, 0, CO, 0>(a);
@@ -350,7 +352,7 @@ static hipError_t by_fmt(const FftLaunch &a) {
 }
 
 hipError_t launch_fft(const FftLaunch &a) {
-    if (a.variant != 1 && a.max_logm == 14 && wide_supported(a.logn)) return launch_fft_wide(a);
+    if (a.variant != 1 && wide_supported(a.logn)) return launch_fft_wide(a);
     if (a.complex_out) {
         if (a.fmt != 3) return hipErrorInvalidValue;
         switch (a.logn) {  // complex output: f32 interleaved only
@@ -360,14 +362,6 @@ hipError_t launch_fft(const FftLaunch &a) {
             RFA_CO(13, 1) RFA_CO(14, 1) RFA_CO(14, 2) RFA_CO(14, 4) RFA_CO(14, 8)
 #undef RFA_CO
         default: return hipErrorInvalidValue;
-        }
-    }
-    if (a.max_logm == 13) {  // experiment: 8K sub-FFTs (2 workgroups per CU) with a wider split
-        switch (a.logn) {
-        case 14: return by_fmt<13, 2, false>(a);
-        case 15: return by_fmt<13, 4, false>(a);
-        case 16: return by_fmt<13, 8, false>(a);
-        default: break;
         }
     }
     switch (a.logn) {
@@ -595,7 +589,11 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     }
 }
 
+#ifdef RFA_AB_BUILD
 static const bool kStateTileOff = std::getenv("RFA_STATE_TILE") && std::atoi(std::getenv("RFA_STATE_TILE")) == 0;
+#else
+static constexpr bool kStateTileOff = false;
+#endif
 
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;

@@ -46,8 +46,6 @@ struct WGeo {
     static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
     static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
     static constexpr int LDS_BYTES = (TW_LDS + SLOTS * HALFP) * 8;
-    // staged kernels: + 16 B for the work-queue slot (next item index)
-    static constexpr int LDS_Q_BYTES = 16;
 };
 
 template <int Q, int LOGM, int PT>
@@ -208,38 +206,20 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // are adjacent in the interleaved window (one 8/16-byte load).  Loads run one
 // chunk ahead of the arithmetic (software pipeline), so a wave keeps two
 // chunks of L2 requests in flight instead of waiting a full round trip per chunk.
-// 64 K, 8-bit input: stage the next frame in two halves, the first right after the
-// pre-stage (exchanges then run in four rounds through a quarter buffer).  1 = on
-// (default, -1..-4 % kernel time, profiles/r02g/split_stage_ab.txt), 0 = whole frame
-// after exchange 1, 2 = first half after exchange 0 (+10 %, not kept), 3 = second half
-// loaded directly by the pre-stage (+5..8 %, not kept, split_direct_ab.txt).
-#ifndef RFA_SPLIT_STAGE
-#define RFA_SPLIT_STAGE 1
-#endif
-// 8/16 K ... 32 K one-residue kernels, 8-bit input: with the exchanges in four rounds
-// through region A the whole next frame fits region B and is staged right after the
-// pre-stage (RFA_SPLIT_WHOLE=1).
-#ifndef RFA_SPLIT_WHOLE
-#define RFA_SPLIT_WHOLE 0
-#endif
+// 64 K, 8-bit input (SPLIT below): the next frame is staged in two halves, the first
+// right after the pre-stage into region B (the exchanges then run in four rounds
+// through the quarter region A), the second after exchange 1 into region A
+// (-1..-4 % kernel time, profiles/r02g/split_stage_ab.txt; the late / direct /
+// whole-frame alternatives measured slower and were removed: split_direct_ab.txt,
+// split_whole_ab.txt).
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
 
-// WP > 0 (RS = 2): the window pairs (w[m], w[m+M]) of the thread's first WP points
-// arrive preloaded in wpre[idx] (issued by the previous item's tail, see
-// fft_wide_kernel); the rest are loaded here, behind the preloaded chunks' work.
-#ifndef RFA_WPRE
-#define RFA_WPRE 0  // measured slower at 8/16/32 (profiles/r02a/window_preload_and_stagger_ab.txt): spills
-#endif
-// PADRAW (fft_w64_kernel): the staged frame sits in LDS as 8 KiB pieces at a
-// 8448-B pitch (one piece per wave region), i.e. raw element e at e + (e >> 12) * 128.
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int WP = 0,
-          bool PADRAW = false, int JS = 0, bool HI_DIRECT = false>
+// JS != 0: the frame's two halves sit JS raw elements apart in LDS (SPLIT staging).
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int JS = 0>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
-                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
-                                         const float2 *wpre = nullptr) {
-    static_assert(WP == 0 || RS == 2, "preloaded window pairs: RS = 2 only");
+                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));  // bytes per sample (per plane)
@@ -274,22 +254,13 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG) {  // frame staged in LDS
-                    if (HI_DIRECT && j >= 1) {  // RFA_SPLIT_STAGE=3: the second half straight from memory
-                        raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
-                    } else {
-                        // JS != 0 (RFA_SPLIT_STAGE): the frame's halves sit JS raw elements apart
-                        const int e = mo + j * (JS != 0 ? JS : M);
-                        raw[s][q][j] = lraw_t[PADRAW ? e + (e >> 12) * 128 : e];
-                    }
+                    raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
             if constexpr (NOWIN) {  // ablation (RFA_DIAG=16): constant window, no window loads
 #pragma unroll
                 for (int j = 0; j < RS; j++) win[s][q][j] = 1.0f / 128.0f;
-            } else if (WP > 0 && c * C + q < WP) {
-                win[s][q][0] = wpre[idx < WP ? idx : 0].x;
-                win[s][q][1] = wpre[idx < WP ? idx : 0].y;
             } else if constexpr (RS == 2) {
                 const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
                 win[s][q][0] = w.x;
@@ -443,22 +414,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
 #else
     constexpr int STG_DIAG_OK = ~48;
 #endif
-    // RFA_SPLIT_STAGE (A/B builds; RS = 2, 8-bit input): the exchanges run in four
-    // rounds through the buffer's first M/4 region A, so the next frame's first half
-    // is staged into region B right after this item's pre-stage (it flies during both
-    // exchanges and passes) and only its second half waits for exchange 1 (into A).
-    constexpr bool SPLIT = RFA_SPLIT_STAGE && STG && RS == 2 && LOGM == 15 && BPS == 2 && !COMPLEX_OUT;
-    // RFA_SPLIT_STAGE=2: exchange 0 keeps two rounds over the whole buffer and the
-    // first half is staged after it (fewer barriers, less time in flight)
-    constexpr bool SPLIT_LATE = SPLIT && RFA_SPLIT_STAGE == 2;
-    // RFA_SPLIT_STAGE=3: only the first half is staged (early); the pre-stage loads the
-    // second half straight from memory (no late DMA to wait for)
-    constexpr bool SPLIT_DIRECT = SPLIT && RFA_SPLIT_STAGE == 3;
+    // SPLIT (RS = 2, 8-bit input): the exchanges run in four rounds through the
+    // buffer's first M/4 region A, so the next frame's first half is staged into
+    // region B right after this item's pre-stage (it flies during both exchanges and
+    // passes) and only its second half waits for exchange 1 (into A).
+    constexpr bool SPLIT = STG && RS == 2 && LOGM == 15 && BPS == 2 && !COMPLEX_OUT;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
-    constexpr bool WHOLE_B = RFA_SPLIT_WHOLE && STG && RS == 1 && LOGM >= 14 && BPS == 2 && !COMPLEX_OUT &&
-                             M * BPS <= (G::HALFP - QP) * 8;
-    constexpr int KR = (SPLIT || WHOLE_B) ? 4 : 2;   // exchange rounds (exchange 1; exchange 0 too unless SPLIT_LATE)
-    constexpr int KR0 = SPLIT_LATE ? 2 : KR;
+    constexpr int KR = SPLIT ? 4 : 2;                // exchange rounds
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
@@ -469,34 +431,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         if constexpr (RS == 1) return u;
         else return (u / (8 * RS)) * 8 + (u & 7);
     };
-    // Work distribution.  Static: items blockIdx.x, +grid, ...  Dynamic (staged
-    // one-residue kernels with a.queue): every workgroup takes its next item from one
-    // device-wide counter a.queue[0], so workgroups that run slow take fewer items
-    // (8 K/16 K: -11 % kernel time).  The index of the next item travels to all waves
-    // through an LDS slot.  The last workgroup to finish (a.queue[1] counts
-    // finishers) zeroes both counters for the next launch.  Two-residue kernels keep
-    // the static stride: it puts the residues of a frame on one XCD (shared L2), which
-    // a single queue does not (+7 % at 64 K, measured).
-    const bool dq = STG && RS == 1 && a.queue != nullptr;
-    int *qslot = reinterpret_cast<int *>(data + G::SLOTS * G::HALFP);
-    auto dequeue = [&]() -> int {
-        const unsigned u = atomicAdd(a.queue, 1u);
-        return u < (unsigned)items ? (int)u : items;
-    };
-    if (a.stagger_ns > 0 && (int)blockIdx.x >= (int)(gridDim.x >> 1)) {
-        // the second half of the grid starts late so workgroups do not all stream HBM
-        // and compute in the same phases (speed only; RFA_STAGGER_NS)
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-        while ((__builtin_amdgcn_s_memrealtime() - t0) * 10ull < (unsigned long long)a.stagger_ns)
-            __builtin_amdgcn_s_sleep(32);
-    }
-    int u0 = blockIdx.x;  // first item of this workgroup
-    if (dq) {
-        if (threadIdx.x == 0) qslot[0] = dequeue();
-        __syncthreads();
-        u0 = qslot[0];
-        __syncthreads();  // every wave has read the slot before it is rewritten
-    }
+    // Work distribution: items blockIdx.x, + grid, ... (static: the residues of a frame
+    // land on blocks b and b + 8, one XCD, so the second residue re-reads the frame from
+    // that XCD's L2; a device-wide work queue measured 7 % slower at 64 K)
+    const int u0 = blockIdx.x;  // first item of this workgroup
     auto next_item = [&](int u) { return u + (int)gridDim.x; };
     // SPLIT: half 0 of a frame goes to region B, half 1 to region A
     auto stage_half = [&](int f, int half) {
@@ -504,17 +442,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             stage_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0),
                                                 half ? buf : buf + QP);
     };
-    auto stage_b = [&](int f) {  // WHOLE_B: the whole frame into region B
-        if constexpr (WHOLE_B) stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride, buf + QP);
-    };
     if constexpr (STG) {
         const int f0 = frame_of(u0);
         if (u0 < items && f0 < a.n_frames) {
-            if constexpr (WHOLE_B) {
-                stage_b(f0);
-            } else if constexpr (SPLIT) {
+            if constexpr (SPLIT) {
                 stage_half(f0, 0);
-                if constexpr (!SPLIT_DIRECT) stage_half(f0, 1);
+                stage_half(f0, 1);
             } else {
                 stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
             }
@@ -538,21 +471,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // staged frame skips them -- vmcnt counts in issue order and they are younger
     // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
     int pending_st = 0;
-    // RS = 2, staged 8/16-bit input: the thread's window pairs are the same for every
-    // item; they are (re)loaded at the tail of each item, after the epilogue has
-    // freed the point registers, so the loads fly during the staged-frame wait
-    constexpr int WP = (STG && RS == 2 && !COMPLEX_OUT && (DIAG & 16) == 0) ? RFA_WPRE : 0;
-    float2 wpre[WP > 0 ? WP : 1];
-    auto load_wpre = [&]() {
-        if constexpr (WP > 0) {
-            const rsrc_t w_rs = make_rsrc(a.window_il, M * RS * 4);
-#pragma unroll
-            for (int idx = 0; idx < WP; idx++)
-                wpre[idx] = buf_load_f32x2(w_rs, tid * 8, (G::TPF * (idx >> 5) + (M / 32) * (idx & 31)) * 8);
-        }
-    };
-    load_wpre();
-    auto body = [&](int u, int &unext) {
+    auto body = [&](int u, int unext) {
         stamp(u, 0);
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
@@ -586,12 +505,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         // ---- pass-0 inputs: x[m], m = tid + TPF*b + (M/32)*t   (b < PT/32, t < 32)
         float2 v[PT];
         using RawT = typename Raw<FMT>::T;
-        const RawT *lraw = reinterpret_cast<const RawT *>((SPLIT || WHOLE_B) ? buf + QP : buf);
+        const RawT *lraw = reinterpret_cast<const RawT *>(SPLIT ? buf + QP : buf);
         if constexpr (STG) {
             // this item's frame, staged by LDS-DMA during the previous item: wait for
             // this wave's pieces, then for every wave's (the barrier)
-            // operations younger than the frame's LDS-DMA: the epilogue stores and the window preloads
-            const int younger = pending_st + WP;
+            // operations younger than the frame's LDS-DMA: the epilogue stores
+            const int younger = pending_st;
             if (younger >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -623,8 +542,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, WP, false, JS, SPLIT_DIRECT>(v, a.window_il, a.wide_tw, in_rs,
-                                                                                        tid, planar, lraw, wpre)
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS>(v, a.window_il, a.wide_tw, in_rs,
+                                                                                       tid, planar, lraw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
@@ -635,24 +554,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if constexpr (!(DIAG & 4)) dft<32>(&v[b * 32]);
         stamp(u, 2);
         if constexpr (STG) {
-            // dynamic queue: thread 0 takes the next item now; the barrier publishes it
-            if (dq && threadIdx.x == 0) qslot[0] = dequeue();
             lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
-            if (dq) unext = qslot[0];
-            if constexpr (SPLIT && !SPLIT_LATE) {  // region B is free until the next item: its half of the next frame now
+            if constexpr (SPLIT) {  // region B is free until the next item: its half of the next frame now
                 const int fn = frame_of(unext);
                 if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
-            if constexpr (WHOLE_B) {  // region B is free until the next item: the whole next frame now
-                const int fn = frame_of(unext);
-                if (unext < items && fn < a.n_frames) stage_b(fn);
-            }
         }
-        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR0>(v, buf, tid);
-        if constexpr (SPLIT_LATE) {  // exchange 0 ended with a barrier after its last reads
-            const int fn = frame_of(unext);
-            if (unext < items && fn < a.n_frames) stage_half(fn, 0);
-        }
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
         if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
@@ -662,10 +570,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // until the next item, so stage the next item's frame now
             const int fn = frame_of(unext);
             if (unext < items && fn < a.n_frames) {
-                if constexpr (SPLIT) {
-                    if constexpr (!SPLIT_DIRECT) stage_half(fn, 1);
-                }
-                else if constexpr (!WHOLE_B) stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
+                if constexpr (SPLIT) stage_half(fn, 1);
+                else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
         if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
@@ -675,10 +581,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             for (int q = 0; q < PT; q++) asm volatile("" : "+v"(v[q].x), "+v"(v[q].y));
         }
 
-        if (!active) {
-            load_wpre();
-            return;
-        }
+        if (!active) return;
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
         // (kernel B of the large-N pair: kk = s + S*(...) with the runtime S = dif_ss and
         // s = dif_r; the stride and frame length below are then uniform runtime values)
@@ -760,21 +663,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             }
             stamp(u, 6);
         }
-        load_wpre();  // next item's window pairs (the point registers are free now)
     };
     for (int u = u0; u < items; it_count++) {
-        int un = dq ? items : next_item(u);  // with the queue, body() dequeues the next item into un
+        const int un = next_item(u);
         body(u, un);
         u = un;
-    }
-    if (dq) {
-        if (threadIdx.x == 0) {
-            __threadfence();  // this workgroup's dequeues are done before it counts itself finished
-            if (atomicAdd(a.queue + 1, 1u) == gridDim.x - 1) {  // last one out: reset for the next launch
-                atomicExch(a.queue, 0u);
-                atomicExch(a.queue + 1, 0u);
-            }
-        }
     }
 }
 
@@ -782,7 +675,7 @@ template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = f
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    const size_t lds = (size_t)G::LDS_BYTES + (STG ? G::LDS_Q_BYTES : 0);
+    const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     static bool attr = false;
     if (!attr) {
@@ -795,7 +688,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int blocks = items;
-    if (a.persist > 0 || STG) {  // persistent: a.persist (STG: all resident) workgroups per CU
+    if (STG) {  // persistent: all resident workgroups
         static int cus = 0, occ = 0;
         if (!cus) {
             int dev = 0;
@@ -805,288 +698,16 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
                                                              lds) != hipSuccess || occ < 1)
                 occ = 1;
         }
-        blocks = std::min(items, cus * (a.persist > 0 ? a.persist : occ));
+        blocks = std::min(items, cus * occ);
     }
-    FftLaunch b = a;
-    if (!STG) b.queue = nullptr;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, b);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(G::THREADS), lds, a.stream, a);
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------
-// N = 64 K "wave" kernel.  The 32 K-point sub-FFT of residue r
-// (same decimation-in-frequency pre-stage as fft_wide_kernel) runs as a four-step
-// 32 x 1024 transform whose 1024-point halves belong to half-waves, so only ONE
-// exchange needs the whole workgroup:
-//   m = m1 + 1024 m2, k = k2 + 32 k1
-//   step 1, thread m1 = tid:  z[k2] = DFT32_m2(y[m1 + 1024 m2]) * W_M^(m1 k2)
-//   exchange 0 (workgroup, two half-rounds): half-wave k2 = tid >> 5 gathers z_m1[k2]
-//   step 2, half-wave k2, lane a = tid & 31, m1 = a + 32 b, k1 = c + 32 d:
-//     pass A: DFT32 over b, * W_1024^(a c); transpose inside the wave through its own
-//     8 KiB of LDS (no s_barrier); pass B: DFT32 over a -> Y[k2 + 32 c + 1024 d] in lane c
-// After its transpose a wave's LDS region is free and the wave stages its 8 KiB
-// piece of the next frame there (LDS-DMA), then writes its outputs: residue r's
-// bins k2 + 32 (c + 32 d) are ring block r + 2 k2 (ring_pos order, logrs 6), so
-// every store instruction covers whole 128-B lines.  Caller rows (natural order)
-// take scattered stores; that path is not the hot one.
-// STATUS: opt-in (RFA_W64=1), measured SLOWER than fft_wide_kernel's residue path
-// (134 vs 95 us per 500 frames, profiles/r02a/w64_wave_kernel_ab.txt): hipcc spills
-// 29-40 dwords per thread here (ScratchSize 116 / 160 B), and every scratch reload
-// behind the epilogue's stores waits for them (vmcnt counts in issue order).  Kept,
-// tested (tests/test_gpu_state.py), for the next attempt at the register budget.
-#ifndef RFA_W64_ABL
-#define RFA_W64_ABL 0  // compile-time ablations (register-pressure study only): 1 no step-1 twiddle,
-                       // 2 no exchange 0, 4 no transpose, 8 no pass-A twiddle, 16 ring-only epilogue
-#endif
-template <int FMT, bool STG>
-__global__ void __launch_bounds__(1024, 4) fft_w64_kernel(FftLaunch a) {
-    constexpr int LOGM = 15, PT = 32, RS = 2;
-    using G = WGeo<LOGM, PT>;
-    constexpr int M = G::M;    // 32768
-    constexpr int n = M * RS;  // 65536
-    constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
-    static_assert(G::TPF == 1024 && G::R1 == 32 && G::R2 == 32, "32 x 32 x 32 plan");
-    static_assert(!STG || n * BPS == 16 * 8192, "staged: one 8 KiB piece of the frame per wave");
-    // per-wave LDS region: 1056 points (8 KiB + 256 B): the wave's staged piece, then
-    // its transposes (two 16 x 33 blocks); 16 regions fill the exchange buffer
-    constexpr int WREG = 1056;
-    static_assert(16 * WREG <= G::HALFP && 16 * 1024 <= G::HALFP, "exchange buffer");
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2 *twp1 = lds;
-    float2 *twp2 = lds + G::TW_P1;
-    float2 *buf = lds + G::TW_LDS;  // 16 K points: staged frame / exchange 0 / per-wave transposes
-    for (int e = threadIdx.x; e < G::TW_LDS; e += 1024) lds[e] = a.wide_tw[e];
-    const int tid = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int items = ((a.n_frames + 7) / 8) * 8 * RS;
-    __syncthreads();  // twiddle tables in LDS
-    if (a.prio && (wave & a.prio)) __builtin_amdgcn_s_setprio(1);
-    // blocks b, b+8, ... share an XCD: a frame's two residues run there (speed only)
-    auto frame_of = [&](int u) { return (u / (8 * RS)) * 8 + (u & 7); };
-    // this wave's 8 KiB piece of a frame's raw bytes into its own region of buf
-    // (1 KiB LDS-DMA per instruction; inline asm for the reason given at stage_frame)
-    auto stage_piece = [&](int f) {
-        if constexpr (STG) {
-            const rsrc_t rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * BPS);
-            const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)(uint8_t *)buf;
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int c = wave * 8 + j;  // 1 KiB piece c of the frame -> this wave's region
-                unsigned keep;
-                asm volatile(
-                    "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                    "buffer_load_dwordx4 %2, %3, %4 offen " STG_POLICY "lds\n\ts_mov_b32 m0, %0"
-                    : "=&s"(keep)
-                    : "s"(base + wave * (WREG * 8) + j * 1024), "v"((tid & 63) * 16), "s"(rs), "s"(c * 1024)
-                    : "memory");
-            }
-        }
-    };
-    const int u0 = blockIdx.x;
-    if (u0 < items && frame_of(u0) < a.n_frames) stage_piece(frame_of(u0));
-    int pending = 0;  // this wave's vector-memory operations issued after its last DMA piece
-    for (int u = u0; u < items; u += gridDim.x) {
-        int z;  // opaque zero: keeps the LDS twiddle reads inside the item loop (VGPR budget)
-        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
-        const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
-        // opaque thread index: every lane-dependent address is rebuilt per item instead of
-        // being hoisted out of the loop into VGPRs that stay live across the whole item
-        int tq;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(tq) : "v"(tid));
-        const int k2 = tq >> 5;   // step-2 sub-FFT of this half-wave
-        const int l32 = tq & 31;  // lane in the half-wave
-        const int g = u / (8 * RS), rem = u - g * (8 * RS);
-        const int r = rem >> 3, frame = g * 8 + (rem & 7);
-        const bool active = frame < a.n_frames;
-        const rsrc_t in_rs =
-            make_rsrc(a.in + (size_t)(active ? frame : 0) * (size_t)a.frame_stride, active ? (unsigned)(n * BPS) : 0u);
-        float2 v[PT];
-        if constexpr (STG) {
-            // every wave's piece of this item's frame has landed
-            if (pending >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (pending >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        }
-        // ---- pre-stage (DIF residue r) + step 1: v[t] = y[tid + 1024 t]
-        using RawT = typename Raw<FMT>::T;
-        [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-            ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, false, 0, true>(v, a.window_il, a.wide_tw, in_rs, tq,
-                                                                             n * 4, reinterpret_cast<const RawT *>(buf))
-                      : void()), ...);
-        }(std::make_integer_sequence<int, RS>{});
-        dft<32>(v);  // z[k2], natural order
-        if constexpr (!(RFA_W64_ABL & 1)) {  // * W_M^(tid k2) = A[tid >> 5][k2] * B[tid & 31][k2] (exact tables)
-            const float2 *ra = tp2 + (tq >> 5) * G::P2_ROW - 1;
-            const float2 *rb = tp2 + G::TW_P2A + (tq & 31) * G::P2_ROW - 1;
-            v[1] = cmul(v[1], cmul(ra[1], rb[1]));
-#pragma unroll
-            for (int t = 2; t < 32; t += 2) {
-                float2 w0 = ra[t], w1 = ra[t + 1];
-                cmul2(w0, rb[t], w1, rb[t + 1]);
-                cmul2(v[t], w0, v[t + 1], w1);
-            }
-        }
-        // ---- exchange 0: buffer [k2][m1 - 512 h] per half-round h (m1 half), 16 K points
-        lds_barrier();  // the staged frame and every wave's previous transpose are consumed
-        // round 0 lands in tmp (v is still live in waves 8..15), round 1 straight in v
-        float2 tmp[16];
-        if constexpr (!(RFA_W64_ABL & 2)) {
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if ((tid >> 9) == h) {  // wave-uniform: waves 8h .. 8h + 7 hold m1 in this half
-                    float2 *w = buf + (tq - 512 * h);
-#pragma unroll
-                    for (int k = 0; k < 32; k++) w[k * 512] = v[k];
-                }
-                lds_barrier();
-                const float2 *rd = buf + k2 * 512 + l32;
-#pragma unroll
-                for (int bb = 0; bb < 16; bb++) {  // m1 = l32 + 32 (16 h + bb)
-                    if (h == 0) tmp[bb] = rd[32 * bb];
-                    else v[16 + bb] = rd[32 * bb];
-                }
-                lds_barrier();
-            }
-#pragma unroll
-            for (int t = 0; t < 16; t++) v[t] = tmp[t];
-        }
-        // ---- step 2, pass A: DFT32 over b, then * W_1024^(a c) (a = l32; table row a)
-        dft<32>(v);
-        if constexpr (!(RFA_W64_ABL & 8)) {
-            const float2 *row = tp1 + l32 * G::P1_ROW - 1;
-            v[1] = cmul(v[1], row[1]);
-#pragma unroll
-            for (int t = 2; t < 32; t += 2) cmul2(v[t], row[t], v[t + 1], row[t + 1]);
-        }
-        // ---- transpose inside the wave, two rounds by a half (a = 16 ar + a'): the writers
-        // (lanes of that half, EXEC-masked) store T[a'][c] at a' * 33 + c, every lane c then
-        // reads its 16 values; the odd pitch keeps both directions conflict free and every
-        // address is a lane base plus an immediate
-        if constexpr (!(RFA_W64_ABL & 4)) {
-            float2 *tw = buf + wave * WREG + ((tq >> 5) & 1) * 528;
-#pragma unroll
-            for (int ar = 0; ar < 2; ar++) {
-                if ((l32 >> 4) == ar) {
-                    float2 *w = tw + (l32 - 16 * ar) * 33;
-#pragma unroll
-                    for (int c = 0; c < 32; c++) w[c] = v[c];
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                const float2 *rd = tw + l32;
-#pragma unroll
-                for (int ap = 0; ap < 16; ap++) {
-                    if (ar == 0) tmp[ap] = rd[ap * 33];
-                    else v[16 + ap] = rd[ap * 33];
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
-#pragma unroll
-            for (int t = 0; t < 16; t++) v[t] = tmp[t];
-        }
-#ifdef RFA_W64_EARLY_DMA
-        // this wave's region is free: stage its piece of the next item's frame
-        {
-            const int un = u + (int)gridDim.x;
-            if (un < items && frame_of(un) < a.n_frames) stage_piece(frame_of(un));
-        }
-#endif
-        // ---- pass B: DFT32 over a -> v[d] = Y[k2 + 32 c + 1024 d], c = l32
-        dft<32>(v);
-        pending = 0;
-        // stage this wave's piece of the next item's frame into its (free) region now,
-        // behind the epilogue's stores' issue: no compiler-placed vmcnt wait of the
-        // epilogue can then end up waiting for the DMA (in issue order it is younger)
-        auto stage_next = [&]() {
-#ifndef RFA_W64_EARLY_DMA
-            const int un = u + (int)gridDim.x;
-            if (un < items && frame_of(un) < a.n_frames) stage_piece(frame_of(un));
-#endif
-        };
-        if (active) {
-        // ---- epilogue (nativedsp.cpp:73-78): bin K = r + 2 (k2 + 32 c + 1024 d); fft-shift
-        // (nativedsp.cpp:77) turns d into d' = (d + 16) mod 32: natural index r + 2 k2 + 64 c + 2048 d',
-        // ring element (r + 2 k2) * 1024 + c + 32 d' (ring_pos, logrs 6)
-        constexpr float db_off = -kDbPerLog2 * (float)(2 * 16);
-        const bool to_ring = a.ring && frame >= a.ring_first;
-        int rr = 0;
-        if (to_ring) {
-            rr = (a.ring_base - frame) % a.ring_rows;
-            if (rr < 0) rr += a.ring_rows;
-        }
-        const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * n + r : nullptr, a.rows ? n * 4 : 0);
-        const rsrc_t ring_rs =
-            make_rsrc(to_ring ? a.ring + (size_t)rr * n + (size_t)r * 1024 : nullptr, to_ring ? n * 4 : 0);
-        const int vo_ring = (2 * k2 * 1024 + l32) * 4, vo_row = (2 * k2 + 64 * l32) * 4;
-        auto epilogue = [&](auto row_c, auto ring_c) {
-#pragma unroll
-            for (int d = 0; d < 32; d++) {
-                const int dp = (d + 16) & 31;
-                const float db = db_unscaled(v[d], db_off);
-                if constexpr (decltype(row_c)::value) buf_store_f32(db, row_rs, vo_row, 2048 * dp * 4);
-                if constexpr (decltype(ring_c)::value) buf_store_f32(db, ring_rs, vo_ring, 32 * dp * 4);
-            }
-        };
-        using T_ = std::true_type;
-        using F_ = std::false_type;
-        if constexpr (RFA_W64_ABL & 16) {
-            if (to_ring) epilogue(F_{}, T_{});
-        } else {
-            if (a.rows && to_ring) epilogue(T_{}, T_{});
-            else if (a.rows) epilogue(T_{}, F_{});
-            else if (to_ring) epilogue(F_{}, T_{});
-        }
-        }
-        stage_next();
-#ifdef RFA_W64_EARLY_DMA
-        pending = (a.rows ? 32 : 0) + (to_ring ? 32 : 0);
-#endif
-    }
-}
-
-template <int FMT, bool STG>
-static hipError_t launch_w64_one(const FftLaunch &a) {
-    using G = WGeo<15, 32>;
-    auto kern = &fft_w64_kernel<FMT, STG>;
-    const size_t lds = (size_t)G::LDS_BYTES;
-    if (!a.wide_tw || !a.window_il) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
-    const int items = ((a.n_frames + 7) / 8) * 8 * 2;
-    if (items <= 0) return hipSuccess;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    }
-    // persistent: one 1024-thread workgroup per CU (LDS and registers), items strided by the grid
-    const int blocks = std::min(items, cus);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(1024), lds, a.stream, a);
-    return hipGetLastError();
-}
-
-static hipError_t launch_w64(const FftLaunch &a) {
-    const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
-    switch (a.fmt) {
-    case 0: return stg ? launch_w64_one<0, true>(a) : launch_w64_one<0, false>(a);
-    case 1: return stg ? launch_w64_one<1, true>(a) : launch_w64_one<1, false>(a);
-    case 2: return launch_w64_one<2, false>(a);
-    case 3: return launch_w64_one<3, false>(a);
-    case 4: return launch_w64_one<4, false>(a);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-int ring_logrs_for(int logn, int wide_big, int w64) {
+int ring_logrs_for(int logn) {
     if (logn > 17 && logn <= kMaxLogN) return logn - kDitLogM;  // large-N kernel B: block s of bins S q + s
     if (!wide_supported(logn) || logn <= 14) return 0;
-    if (logn == 16 && wide_big == 15 && w64) return 6;
-    return logn - wide_logm(logn, wide_big);
+    return logn - wide_logm(logn);
 }
 
 template <int LOGM, int PT, int RS, bool CO>
@@ -1147,6 +768,7 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
 
 hipError_t launch_fft_wide(const FftLaunch &a) {
     const bool co = a.complex_out != nullptr;
+#ifdef RFA_AB_BUILD
     if (a.diag == 16 && a.logn == 16) {  // staged 64 K kernel without window loads (profiling only)
         if (a.fmt != 0 || co) return hipErrorInvalidValue;
         return launch_wide_one<15, 32, 2, 0, false, 16, true>(a);
@@ -1182,26 +804,17 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         default: return hipErrorInvalidValue;
         }
     }
+#endif
     if (a.fmt == kFmtDif) {  // kernel B of the large-N pair (dB rows / ring, or the ordered spectrum)
         if (a.dif_ss < 8 || a.dif_ss > 32) return hipErrorInvalidValue;
         return co ? launch_wide_one<kDitLogM, 32, 1, kFmtDif, true>(a) : launch_wide_one<kDitLogM, 32, 1, kFmtDif, false>(a);
     }
-    if (a.logn >= 15 && a.wide_big == 15) {
-        switch (a.logn) {
-        case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
-        case 16:
-            if (!co && a.w64) return launch_w64(a);
-            return co ? wide_by_fmt<15, 32, 2, true>(a) : wide_by_fmt<15, 32, 2, false>(a);
-        case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
-        default: return hipErrorInvalidValue;
-        }
-    }
     switch (a.logn) {
     case 13: return co ? wide_by_fmt<13, 32, 1, true>(a) : wide_by_fmt<13, 32, 1, false>(a);
     case 14: return co ? wide_by_fmt<14, 32, 1, true>(a) : wide_by_fmt<14, 32, 1, false>(a);
-    case 15: return co ? wide_by_fmt<14, 32, 2, true>(a) : wide_by_fmt<14, 32, 2, false>(a);
-    case 16: return co ? wide_by_fmt<14, 32, 4, true>(a) : wide_by_fmt<14, 32, 4, false>(a);
-    case 17: return co ? wide_by_fmt<14, 32, 8, true>(a) : wide_by_fmt<14, 32, 8, false>(a);
+    case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
+    case 16: return co ? wide_by_fmt<15, 32, 2, true>(a) : wide_by_fmt<15, 32, 2, false>(a);
+    case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
     default: return hipErrorInvalidValue;
     }
 }

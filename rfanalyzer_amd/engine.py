@@ -96,6 +96,13 @@ class SpectrumEngine:
                                                 out.ctypes.data if rows else None), "rfa_process_host")
         return out
 
+    def process_batches(self, in_ptr: int, n_batches: int, batch_stride: int, frames_per_batch: int,
+                        frame_stride: int = 0, rows_ptr: int | None = None) -> None:
+        """rfa_process_batches: n_batches consecutive rfa_process calls in one enqueue
+        (one kernel launch when the batches are packed).  Device pointers, async."""
+        self._check(_lib.lib().rfa_process_batches(self._h, in_ptr, n_batches, batch_stride, frames_per_batch,
+                                                   frame_stride, rows_ptr), "rfa_process_batches")
+
     def push_packet(self, packet, frequency: int, sample_rate: int, row: bool = False):
         """One raw packet through the reference's framing (rfa_push_packet,
         Scheduler.kt:252-273): fills the partial frame, processes it once complete.

@@ -38,6 +38,12 @@ def test_gpus_2_spawns_two_ranks_that_agree(mode):
     assert out["ms_per_step"] >= 2.0
     assert out["scaling"] == ("weak" if mode == "streams" else "strong")
     assert out["config"]["parallelism"] == f"{mode}2"
+    if mode == "streams":
+        # the other BASELINE configs ride along in multi-GPU runs, each with every rank's time
+        for key in ("config2", "config4", "config5", "f32"):
+            assert key in out, key
+            assert len(out[key]["per_rank_s"]) == 2, key
+        assert out["config4"]["scaling"] == "strong" and out["config5"]["scaling"] == "weak"
 
 
 def test_world_size_mismatch_is_an_error():

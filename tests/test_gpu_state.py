@@ -241,36 +241,6 @@ def test_config3_state_at_size(rfa, n, ring_rows, batches):
                 assert np.all(ring[[(-g) % ring_rows for g in range(f, ring_rows)]] == -9999)
 
 
-@pytest.mark.parametrize("parts,join,groups", [
-    (2, "eager", ((137,), (100,), (400,), (500,))),
-    (2, "lazy", ((137, 100), (400, 500, 250))),   # back-to-back batches, joined at the reads
-    (4, "lazy", ((500, 500), (63, 300))),        # 4 parts of 125 / 75; 63 runs unsplit (parts < 32)
-])
-def test_config3_state_overlap(rfa, monkeypatch, parts, join, groups):
-    """RFA_STATE_OVERLAP: the ring-resident batch as frame parts whose peak / EMA update
-    runs on a second stream beside the next part's FFT (engine.hip process_impl).  Same
-    ring / peaks / EMA as the restatement, with lazy joins across consecutive batches."""
-    monkeypatch.setenv("RFA_STATE_OVERLAP", str(parts))
-    monkeypatch.setenv("RFA_STATE_JOIN", join)
-    n, ring_rows, alpha = 65536, 500, 0.1
-    data, rows = _cfg3_rows(n, 1400, 5)  # one oracle pass shared by the three cases
-    fb = 2 * n
-    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=alpha, peak_hold=True,
-                            ring_rows=ring_rows) as e:
-        e.set_tuning(433_920_000, 20_000_000)
-        f = 0
-        for g in groups:
-            for b in g:
-                e.process(data[f * fb:(f + b) * fb], b, rows=False)
-                f += b
-            assert gu.db_diff(e.peaks(), rows[:f].max(0)) <= gu.DB_TOL, (g, f)
-            assert gu.db_diff(e.ema(), processor.ema_batch(rows[:f], alpha)) <= gu.DB_TOL, (g, f)
-            ring, ri, wi = e.ring()
-            assert ri == (-(f - 1)) % ring_rows and wi == (-f) % ring_rows
-            live = list(range(max(0, f - ring_rows), f))
-            assert gu.db_diff(ring[[(-g_) % ring_rows for g_ in live]], rows[live]) <= gu.DB_TOL
-
-
 @pytest.mark.parametrize("n,batches", [(262144, (3, 9, 2)), (524288, (5, 6)), (1048576, (1, 7, 4))])
 def test_column_order_ring_state_tiles(rfa, n, batches):
     """N >= 256 K keeps the ring in column order (RS = N / 32 K blocks); the peak / EMA
@@ -355,25 +325,64 @@ def test_fft_size_change_restarts_ring_and_peaks(rfa, na, nb):
         assert gu.db_diff(e.ema(), processor.ema_batch(rows_b, 0.25)) <= gu.DB_TOL
 
 
-def test_w64_wave_kernel_opt_in(rfa, monkeypatch):
-    """RFA_W64=1 selects the four-step wave kernel at N = 64 K (fft_wide.hip, opt-in):
-    ring order 64 (ring_pos logrs 6), rows / ring / peaks / EMA / boxcar equal the
-    restatement as with the default kernel."""
-    monkeypatch.setenv("RFA_W64", "1")
-    n, frames, rows_r = 65536, 40, 30
-    data, ref = _cfg3_rows(n, frames, 7)
-    with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=0.1, peak_hold=True, ring_rows=rows_r) as e:
-        assert e.ring_order == 64
-        e.set_tuning(433_920_000, 20_000_000)
-        rows = e.process(data[: 10 * 2 * n], 10)           # caller rows (natural order) + ring
-        assert gu.db_diff(rows, ref[:10]) <= gu.DB_TOL
-        e.process(data[10 * 2 * n:], frames - 10, rows=False)  # ring only (the hot path)
-        assert gu.db_diff(e.peaks(), ref.max(0)) <= gu.DB_TOL
-        assert gu.db_diff(e.ema(), processor.ema_batch(ref, 0.1)) <= gu.DB_TOL
-        ring, ri, _ = e.ring()
-        newest = [(ri + k) % rows_r for k in range(rows_r)]
-        assert gu.db_diff(ring[newest], ref[::-1][:rows_r]) <= gu.DB_TOL
-        p = processor.FftProcessorRef(n, rows_r)
-        for r in ref:
-            p.push(r, 433_920_000, 20_000_000)
-        assert gu.db_diff(e.boxcar(3), p.boxcar(3)) <= gu.DB_TOL
+def test_state_generation_tracks_device_pointers(rfa):
+    """rfa_get_device_state pointers are valid while rfa_get_state_generation is
+    unchanged: a shifting retune swaps the ring buffer, a resize and an FFT-size change
+    reallocate; an unchanged tuning or a plain batch keeps them."""
+    import ctypes
+    n = 1024
+    data = np.random.default_rng(2).integers(-128, 128, size=2 * n * 4, dtype=np.int8).tobytes()
+    with rfa.SpectrumEngine(n, "blackman", "s8", peak_hold=True, ring_rows=4) as e:
+        lib = rfa.lib()
+
+        def ptrs():
+            r, p, m = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+            assert lib.rfa_get_device_state(e.handle, ctypes.byref(r), ctypes.byref(p), ctypes.byref(m)) == 0
+            return r.value, p.value
+        e.set_tuning(100_000_000, 2_000_000)
+        e.process(data, 2, rows=False)
+        g0, p0 = e.state_generation(), ptrs()
+        e.set_tuning(100_000_000, 2_000_000)
+        e.process(data, 2, rows=False)
+        assert (e.state_generation(), ptrs()) == (g0, p0)
+        e.set_tuning(100_001_000, 2_000_000)  # shift: the ring moves to the other buffer
+        g1 = e.state_generation()
+        assert g1 > g0 and ptrs()[0] != p0[0]
+        e.set_ring_rows(6)
+        e.process(data, 1, rows=False)         # the resize is applied with the next frame
+        g2 = e.state_generation()
+        assert g2 > g1
+        e.set_fft_size(2048)
+        assert e.state_generation() > g2
+
+
+@pytest.mark.parametrize("packed", [True, False])
+def test_process_batches_equals_consecutive_calls(rfa, packed):
+    """rfa_process_batches (config 4's multi-batch enqueue) is exactly n_batches
+    consecutive rfa_process calls: rows bit-identical, same ring, peaks and EMA;
+    packed batches take one launch, strided ones one per batch."""
+    import torch
+    n, fpb, nb = 8192, 12, 5
+    gap = 0 if packed else 3 * 2 * n  # strided: 3 unused frames between batches
+    stride_b = fpb * 2 * n + gap
+    raw = np.random.default_rng(31).integers(-128, 128, size=nb * stride_b, dtype=np.int8)
+    dev = torch.from_numpy(raw.view(np.uint8).copy()).cuda()
+    kw = dict(avg="ema", ema_alpha=0.2, peak_hold=True, ring_rows=40)
+    with rfa.SpectrumEngine(n, "blackman", "s8", **kw) as a, rfa.SpectrumEngine(n, "blackman", "s8", **kw) as b:
+        for e in (a, b):
+            e.set_tuning(100_000_000, 2_000_000)
+        rows_a = torch.empty((nb * fpb, n), dtype=torch.float32, device="cuda")
+        a.process_batches(dev.data_ptr(), nb, stride_b, fpb, 0, rows_a.data_ptr())
+        a.synchronize()
+        rows_b = []
+        for k in range(nb):
+            rows_b.append(b.process(raw[k * stride_b:k * stride_b + fpb * 2 * n].tobytes(), fpb))
+        np.testing.assert_array_equal(rows_a.cpu().numpy(), np.concatenate(rows_b))
+        ra, ria, wia = a.ring()
+        rb, rib, wib = b.ring()
+        assert (ria, wia) == (rib, wib)
+        np.testing.assert_array_equal(ra, rb)
+        np.testing.assert_array_equal(a.peaks(), b.peaks())
+        # the EMA recursion is re-associated by the chunked scan (one batch of 60 frames
+        # vs five of 12): equal to fp32 rounding, not bit for bit
+        np.testing.assert_allclose(a.ema(), b.ema(), rtol=0, atol=2e-4)
