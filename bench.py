@@ -455,8 +455,11 @@ def cpu_baseline(args, n, seconds):
     import oracle
 
     hinfo = host_info()
-    # every CPU of the affinity mask, capped at 256 threads (the GPU boxes limit tasks per job)
-    threads = max(1, min(256, hinfo.get("affinity_cpus") or 1))
+    # every CPU this process may use: the affinity mask, bounded by the cgroup CPU quota
+    # when one is set (more threads than the quota only time-slice the same CPUs)
+    cpus = hinfo.get("affinity_cpus") or 1
+    quota = hinfo.get("cgroup_cpu_quota")
+    threads = max(1, min(256, cpus, int(quota) if quota else cpus))
 
     fmt = {"s8": 0, "f32": 3}.get(args.format, 0)
     frames = max(1, (8 * 2 ** 20) // (n * 8))  # ~8 MB sample, processed repeatedly
@@ -510,8 +513,8 @@ def cpu_baseline(args, n, seconds):
             t.join()
         el = max(r[1] for r in res)
         out["multi_core"] = {"value": round(sum(r[0] for r in res) * n / el / 1e6, 3), "cores": threads,
-                             "sample": f"{threads} threads (every CPU in this process's affinity mask) x the "
-                                       f"same loop for {el:.1f} s"}
+                             "sample": f"{threads} threads (every CPU this process may use: affinity mask "
+                                       f"{cpus}, cgroup quota {quota}) x the same loop for {el:.1f} s"}
     return out
 
 

@@ -264,14 +264,18 @@ RFA_API int rfa_get_state_generation(const rfa_handle *h, int64_t *generation);
 
 /* Storage order of the device ring rows (no reference counterpart: the JVM
  * waterfallBuffer rows are natural order, FftProcessor.kt:222-227, and
- * rfa_get_ring returns them so).  *residues = RS: fft-shifted bin t of a device
- * ring row lives at element (t mod RS) * (N/RS) + t / RS.  RS = 1 is natural
- * order; the N = 64 K / 128 K kernels compute a frame as RS residue sub-FFTs and
- * store each residue's bins as one contiguous block (whole cache lines per
- * workgroup); N = 256 K .. 1 M use RS = N / 32768 (the large-N kernel B writes
- * the bins S q + s of column s as block s).  Every rfa_* consumer of the ring
- * handles this internally. */
+ * rfa_get_ring returns them so).  *residues = RS: the fft-shifted bin t of a
+ * device ring row lives in block t mod RS of N/RS elements.  RS = 1 is one block;
+ * the N = 64 K / 128 K kernels compute a frame as RS residue sub-FFTs and store
+ * each residue's bins as one block (whole cache lines per workgroup); N = 256 K ..
+ * 1 M use RS = N / 32768 (the large-N kernel B writes the bins S q + s of column
+ * s as block s).  Inside a block, N = 32 K .. 128 K keep the 32 K-point kernel's
+ * store tiles (16-B stores per lane); N = 256 K .. 1 M and N <= 16 K natural
+ * order (bin t at block offset t / RS).  rfa_get_ring_positions fills the
+ * storage position of every fft-shifted bin (positions[N]) for zero-copy
+ * consumers; every rfa_* consumer of the ring handles the order internally. */
 RFA_API int rfa_get_ring_order(const rfa_handle *h, int32_t *residues);
+RFA_API int rfa_get_ring_positions(const rfa_handle *h, int32_t *positions, size_t count);
 
 /* Reference-seam entry points (host arrays, synchronous).  They use the
  * handle's N; the window/format of the handle are ignored where the reference

@@ -108,6 +108,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_set_fft_size": (ctypes.c_int, [_h, ctypes.c_int32]),
         "rfa_get_device_state": (ctypes.c_int, [_h, ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp)]),
         "rfa_get_ring_order": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_get_ring_positions": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t]),
         "rfa_stream_copy": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp]),
         "rfa_ddc_get_format": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32)]),
         "rfa_windowed_fft_mag_planar": (ctypes.c_int, [_h, _fp, _fp, _fp, ctypes.c_size_t]),

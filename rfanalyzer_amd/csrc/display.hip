@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
     if (i >= a.width) return;
     const int buffer_index = sel.y;
     const float *row = a.ring + (size_t)buffer_index * a.n;
-    const int lm = (31 - __clz(a.n)) - a.ring_logrs;  // ring storage order (ring_pos)
+    const int lm = ring_logm(a.ring_logrs, 31 - __clz(a.n));  // ring storage order (ring_pos)
     unsigned *out = a.colors + (size_t)buffer_index * a.width + i;
     if (i >= a.first_pixel + 1 && i < a.last_pixel - 1) {
         const bool peaks_here = row_number == 0 && a.peaks_y;
@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(256) row_window_kernel(const float *row, int l
                                                          const int *hi, int count, float *peak, float *avg) {
     const int w = blockIdx.x;
     if (w >= count) return;
-    const int lm = (31 - __clz(n)) - logrs;  // ring storage order (ring_pos)
+    const int lm = ring_logm(logrs, 31 - __clz(n));  // ring storage order (ring_pos)
     const int a = lo[w], b = hi[w];
     float mx = -INFINITY;
     bool nan = false;

@@ -33,7 +33,8 @@ struct rfa_handle {
     float *d_window = nullptr;
     float *d_window_none = nullptr;   // all ones (already-windowed f32 seams)
     float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
-    float *d_window_il = nullptr;     // N > 16384: scaled window as [m][j], m < 16384, j < N/16384
+    float *d_window_il = nullptr;     // N > 32768: scaled window as [m][j], m < 32768, j < N/32768
+    float4 *d_window_cw = nullptr;    // N = 65536: (w[m] W_N^m, -w[m+M] W_N^m), residue 1 of the pre-stage
     float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17, and kernel A for larger N)
     // N = 2^18..2^20 (decimation in frequency, fft_large.hip)
     float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{m s} = C[s][m >> 7] * D[s][m & 127]
@@ -286,7 +287,10 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     }
     a.wide_tw = h->d_wide_tw;
     a.variant = h->variant;
-    if (a.window == h->d_window) a.window_il = h->d_window_il;
+    if (a.window == h->d_window) {
+        a.window_il = h->d_window_il;
+        a.window_cw = h->d_window_cw;
+    }
     else if (h->logn > 14) a.variant = 1;  // seam windows have no interleaved copy: narrow kernel
     // the ring order is a property of the wide kernel's residue split (ring_pos)
     if (a.ring && h->ring_logrs && a.variant == 1 && h->logn <= 17)
@@ -448,6 +452,19 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (hipMalloc(&h->d_window_il, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_window_il, il.data(), n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess)
             return bail(RFA_ERR_HIP);
+        if (rs == 2) {  // residue 1's complex window (fft_wide.hip prestage CW): products in double, rounded once
+            const std::vector<float> wd = make_window(n, cfg->window);
+            std::vector<float4> cw((size_t)m_sub);
+            for (int m = 0; m < m_sub; m++) {
+                const double sc = (double)scale, ang = -2.0 * M_PI * (double)m / (double)n;
+                const double c = std::cos(ang), s = std::sin(ang);
+                const double w0 = (double)wd[m] * sc, w1 = (double)wd[(size_t)m + m_sub] * sc;
+                cw[m] = make_float4((float)(w0 * c), (float)(w0 * s), (float)(-w1 * c), (float)(-w1 * s));
+            }
+            if (hipMalloc(&h->d_window_cw, cw.size() * sizeof(float4)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+            if (hipMemcpy(h->d_window_cw, cw.data(), cw.size() * sizeof(float4), hipMemcpyHostToDevice) != hipSuccess)
+                return bail(RFA_ERR_HIP);
+        }
     }
     if (logn > 17) {  // decimation in frequency: S column DFTs, then S sub-FFTs of M = 32768 points
         std::vector<float2> c, d, blob = rfa::wide_twiddles(rfa::kDitLogM, rfa::kWidePT, rfa::kDitLogM);
@@ -540,6 +557,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_window_none);
     hipFree(h->d_window_black);
     hipFree(h->d_window_il);
+    hipFree(h->d_window_cw);
     hipFree(h->d_wide_tw);
     hipFree(h->d_dit_c);
     hipFree(h->d_dit_d);
@@ -1119,13 +1137,21 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
 
 int rfa_get_ring_order(const rfa_handle *h, int32_t *residues) {
     if (!h || !residues) return RFA_ERR_INVALID;
-    *residues = 1 << h->ring_logrs;
+    *residues = 1 << rfa::ring_lr(h->ring_logrs);
     return RFA_OK;
 }
 
 int rfa_get_state_generation(const rfa_handle *h, int64_t *generation) {
     if (!h || !generation) return RFA_ERR_INVALID;
     *generation = h->generation;
+    return RFA_OK;
+}
+
+int rfa_get_ring_positions(const rfa_handle *h, int32_t *positions, size_t count) {
+    if (!h || (!positions && count)) return RFA_ERR_INVALID;
+    if (count != (size_t)h->n) return fail(const_cast<rfa_handle *>(h), RFA_ERR_SIZE, "positions must hold fft_size entries");
+    const int lm = rfa::ring_logm(h->ring_logrs, h->logn);
+    for (int t = 0; t < h->n; t++) positions[t] = rfa::ring_pos(t, h->ring_logrs, lm);
     return RFA_OK;
 }
 

@@ -108,6 +108,25 @@ RFA_HD void cmul2(float2 &a0_, float2 w0_, float2 &a1_, float2 w1_) {
 #endif
 }
 
+// a0 * w0 + a1 * w1 (complex), four packed instructions: the residue-1 pre-stage of
+// the 64 K kernel with the twiddle folded into a complex window (fft_wide.hip)
+RFA_HD float2 cmac2(float2 a0_, float2 w0_, float2 a1_, float2 w1_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const f2v a0 = to_v(a0_), w0 = to_v(w0_), a1 = to_v(a1_), w1 = to_v(w1_);
+    f2v m, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(m) : "v"(a0), "v"(w0));  // (a0.x w0.x, a0.x w0.y)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a0), "v"(w0), "v"(m));  // + (a0.y (-w0.y), a0.y w0.x)
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(m) : "v"(a1), "v"(w1), "v"(r));  // + a1.x w1
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a1), "v"(w1), "v"(m));  // + (a1.y (-w1.y), a1.y w1.x)
+    return from_v(r);
+#else
+    return make_float2(a0_.x * w0_.x - a0_.y * w0_.y + a1_.x * w1_.x - a1_.y * w1_.y,
+                       a0_.x * w0_.y + a0_.y * w0_.x + a1_.x * w1_.y + a1_.y * w1_.x);
+#endif
+}
+
 // complex a * (c, s) for a compile-time constant (held in an SGPR pair)
 // (plain vector code: both constant pairs live in SGPRs, hipcc emits v_pk_mul +
 // v_pk_fma and is free to interleave independent multiplies)
@@ -411,6 +430,22 @@ __device__ __forceinline__ float2 buf_load_f32x2(rsrc_t rs, int voff, int soff) 
 }
 __device__ __forceinline__ void buf_store_f32(float x, rsrc_t rs, int voff, int soff) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), rs, voff, soff, 0);
+}
+// 16-B store.  Inline asm with a trailing s_nop: a VALU write to the data VGPRs of a
+// just-issued buffer store of more than 64 bits needs a wait state, and hipcc (ROCm
+// 7.2, gfx950) let the next v_pk_fma overwrite them back to back -- the last lanes of
+// each 16-lane group then stored the new values (measured: ~1/16 of the 64 K ring's
+// bins wrong).  The asm block keeps the store and its nop together.
+__device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float d, rsrc_t rs, int voff, int soff) {
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    i32x4 v = {__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), __builtin_bit_cast(int, c),
+               __builtin_bit_cast(int, d)};
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs), "s"(soff)
+                 : "memory");
+#else
+    (void)v; (void)rs; (void)voff; (void)soff;
+#endif
 }
 __device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, int soff) {
     typedef int i32x2 __attribute__((ext_vector_type(2)));

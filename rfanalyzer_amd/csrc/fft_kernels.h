@@ -16,12 +16,32 @@ namespace rfa {
 // residue workgroup writes whole cache lines.  logrs = 0 is natural order.  Only
 // the device ring uses this order; caller rows, peaks, EMA and every host copy
 // are in natural order (ring consumers gather through ring_pos).
-__host__ __device__ __forceinline__ int ring_pos(int t, int logrs, int logm) {
-    return ((t & ((1 << logrs) - 1)) << logm) | (t >> logrs);
+//
+// Order code (engine ring_logrs, FftLaunch / StateLaunch / DrawLaunch ring_logrs):
+// bits 0-7 logrs; bit 8 (kRingTile, M = 32 K blocks only) additionally permutes the
+// M elements of each block into the wide kernel's store tiles, so its epilogue
+// writes 16 B per lane (8 x dwordx4 per thread instead of 32 x dword): sub-position
+// i' = t'*1024 + w*64 + l (thread 64 w + l of the 1024-thread sub-FFT, its output
+// t' = 0..31 after the fft-shift) lives at w*2048 + (t' >> 2)*256 + l*4 + (t' & 3)
+// -- a bit permutation, so every consumer below maps with ring_pos / ring_bin.
+constexpr int kRingTile = 0x100;
+__host__ __device__ __forceinline__ int ring_lr(int code) { return code & 0xff; }
+// logm of a ring of 2^logn bins in order `code`
+__host__ __device__ __forceinline__ int ring_logm(int code, int logn) { return logn - (code & 0xff); }
+__host__ __device__ __forceinline__ int tile_pos(int i) {  // i' -> storage position (M = 32 K)
+    return (((i >> 6) & 15) << 11) | ((i >> 12) << 8) | ((i & 63) << 2) | ((i >> 10) & 3);
+}
+__host__ __device__ __forceinline__ int tile_sub(int p) {  // inverse of tile_pos
+    return ((((p >> 8) & 7) << 2 | (p & 3)) << 10) | ((p >> 11) << 6) | ((p >> 2) & 63);
+}
+__host__ __device__ __forceinline__ int ring_pos(int t, int code, int logm) {
+    const int lr = code & 0xff, sub = t >> lr;
+    return ((t & ((1 << lr) - 1)) << logm) | ((code & kRingTile) ? tile_pos(sub) : sub);
 }
 // inverse: the natural (fft-shifted) bin stored at ring element p
-__host__ __device__ __forceinline__ int ring_bin(int p, int logrs, int logm) {
-    return ((p & ((1 << logm) - 1)) << logrs) | (p >> logm);
+__host__ __device__ __forceinline__ int ring_bin(int p, int code, int logm) {
+    const int lr = code & 0xff, q = p & ((1 << logm) - 1);
+    return (((code & kRingTile) ? tile_sub(q) : q) << lr) | (p >> logm);
 }
 
 // Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
@@ -39,6 +59,9 @@ struct FftLaunch {
     int logn = 0;  // N = 1 << logn
     const float *window = nullptr;  // N floats (device); all ones for RFA_WINDOW_NONE
     const float *window_il = nullptr;  // N > M: window[m + j*M] at [m*RS + j] (wide kernel pre-stage)
+    // N = 64 K, residue 1 of the pre-stage: the twiddle folded into a complex window,
+    // [m] = (w[m] W_N^m, -w[m + M] W_N^m) as float4, m < M (null: separate twiddle)
+    const float4 *window_cw = nullptr;
     // wide kernel twiddle blob (exact, from double): pass-1 [32][R1] | pass-2 A,B [16][16] |
     // pre-stage pre_a [RS][512] | pre_b [RS][32]   (DESIGN.md "Twiddles")
     const float2 *wide_tw = nullptr;  // wide_twiddles() blob (layout in fft_wide.hip WGeo)

@@ -406,7 +406,7 @@ __device__ __forceinline__ int ilog2_dev(int n) { return 31 - __clz(n); }
 __global__ void state_kernel(StateLaunch a) {
     const int pos = blockIdx.x * blockDim.x + threadIdx.x;  // storage position
     if (pos >= a.n) return;
-    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ilog2_dev(a.n) - lr);
+    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ring_logm(lr, ilog2_dev(a.n)));
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     const float al = a.ema_alpha;
@@ -524,7 +524,7 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
 __global__ void state_combine_kernel(StateLaunch a, int chunks) {
     const int pos = blockIdx.x * blockDim.x + threadIdx.x;  // storage position of the partials
     if (pos >= a.n) return;
-    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ilog2_dev(a.n) - lr);
+    const int lr = state_logrs(a), bin = ring_bin(pos, lr, ring_logm(lr, ilog2_dev(a.n)));
     float pk = a.peaks ? a.peaks[bin] : 0.f;
     float em = a.ema ? a.ema[bin] : 0.f;
     for (int c = 0; c < chunks; c++) {
@@ -573,7 +573,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
 #pragma unroll
     for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
     __syncthreads();
-    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
+    const int lr = state_logrs(a), lm = ring_logm(lr, ilog2_dev(a.n));
     for (int i = threadIdx.x; i < BPB; i += 256) {
         const int gb = ring_bin(blockIdx.x * BPB + i, lr, lm);  // natural bin of storage position
         float p = a.peaks ? a.peaks[gb] : 0.f;
@@ -598,7 +598,7 @@ static constexpr bool kStateTileOff = false;
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
     const int tpb = 256;
-    if (a.ring_rows > 0 && a.ring_logrs >= 3 && a.ring_logrs <= 5 && !kStateTileOff) {
+    if (a.ring_rows > 0 && !(a.ring_logrs & kRingTile) && a.ring_logrs >= 3 && a.ring_logrs <= 5 && !kStateTileOff) {
         // column-order ring (N >= 256 K): tiled sequential update (RFA_STATE_TILE=0: A/B off)
         const int m = a.n >> a.ring_logrs;
         if (m % 64 == 0) {
@@ -641,7 +641,7 @@ __global__ void __launch_bounds__(64) channel_mean_kernel(StateLaunch a, int fir
     const int f = blockIdx.x * 64 + threadIdx.x;
     if (f >= a.n_frames) return;
     const float *row = state_row(a, f);
-    const int lr = state_logrs(a), lm = ilog2_dev(a.n) - lr;
+    const int lr = state_logrs(a), lm = ring_logm(lr, ilog2_dev(a.n));
     float s = 0.0f;
 #pragma unroll 8
     for (int i = first; i < last; i++) s += row[ring_pos(i, lr, lm)];
@@ -672,7 +672,7 @@ hipError_t launch_fill(float *p, long long count, float value, hipStream_t s) {
 // i addressed through the ring's storage order (ring_pos)
 __global__ void ring_shift_kernel(const float *src, float *dst, int n, int logrs, int shift, float fill) {
     const int row = blockIdx.y;
-    const int lm = ilog2_dev(n) - logrs;
+    const int lm = ring_logm(logrs, ilog2_dev(n));
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const int s = i - shift;
         dst[(size_t)row * n + ring_pos(i, logrs, lm)] =
@@ -691,7 +691,7 @@ hipError_t launch_ring_shift(const float *src, float *dst, int rows, int n, int 
 
 __global__ void ring_natural_kernel(const float *src, float *dst, int n, int logrs) {
     const int row = blockIdx.y;
-    const int lm = ilog2_dev(n) - logrs;
+    const int lm = ring_logm(logrs, ilog2_dev(n));
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
         dst[(size_t)row * n + i] = src[(size_t)row * n + ring_pos(i, logrs, lm)];
 }
@@ -730,7 +730,7 @@ hipError_t launch_ring_rotate(const float *src, int src_rows, float *dst, int ds
 __global__ void boxcar_kernel(const float *ring, int rows, int n, int logrs, int read_index, int length, float *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const int p = ring_pos(i, logrs, ilog2_dev(n) - logrs);
+    const int p = ring_pos(i, logrs, ring_logm(logrs, ilog2_dev(n)));
     float acc = 0.f;
     for (int r = 0; r <= length; r++) acc += ring[(size_t)((read_index + r) % rows) * n + p];
     out[i] = acc / (float)(length + 1);

@@ -84,6 +84,26 @@ template <typename T>
 __device__ __forceinline__ T *lds_opaque(T *p) { return p; }  // host pass: never executed
 #endif
 
+// one float2 as its own ds_read_b64: a volatile LDS access keeps hipcc from fusing
+// neighbours into ds_read2_b64, which moves half the bytes per LDS cycle on gfx950
+// (MI355X_MICROARCH.md, LDS table: 8 cycles per ds_read2_b64 vs 2 per ds_read_b64)
+__device__ __forceinline__ float2 lds_ld2(const float2 *p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return from_v(*(const volatile __attribute__((address_space(3))) f2v *)(p));
+#else
+    return *p;
+#endif
+}
+
+#ifndef RFA_TWREAD1
+#define RFA_TWREAD1 1  // pass-1/2 twiddle reads as single ds_read_b64 (A/B builds: 0 = hipcc fuses read2)
+#endif
+template <typename T>
+__device__ __forceinline__ float2 tw_ld(const T *p) {
+    if constexpr (RFA_TWREAD1) return lds_ld2(p);
+    else return *p;
+}
+
 template <int Q, int LOGM, int PT, int KR = 2>
 __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
     // KR rounds (2: the M/2 buffer; 4: an M/4 buffer, RFA_SPLIT_STAGE) -- round h
@@ -142,9 +162,10 @@ __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *tw
     const float2 *row = twp1 + (tid & 31) * WGeo<LOGM, PT>::P1_ROW - 1;
 #pragma unroll
     for (int b = 0; b < W::NB; b++) {
-        v[b * W::R + 1] = cmul(v[b * W::R + 1], row[1]);
+        v[b * W::R + 1] = cmul(v[b * W::R + 1], tw_ld(row + 1));
 #pragma unroll
-        for (int t = 2; t < W::R; t += 2) cmul2(v[b * W::R + t], row[t], v[b * W::R + t + 1], row[t + 1]);
+        for (int t = 2; t < W::R; t += 2)
+            cmul2(v[b * W::R + t], tw_ld(row + t), v[b * W::R + t + 1], tw_ld(row + t + 1));
     }
 #pragma unroll
     for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
@@ -174,14 +195,14 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
     const float2 *ra = twp2 + (tid / G::LO) * G::P2_ROW - 1;
     const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
     {
-        const float2 w1 = cmul(ra[1], rb[1]);
+        const float2 w1 = cmul(tw_ld(ra + 1), tw_ld(rb + 1));
 #pragma unroll
         for (int b = 0; b < W::NB; b++) v[b * R2 + 1] = cmul(v[b * R2 + 1], w1);
     }
 #pragma unroll
     for (int t = 2; t < R2; t += 2) {  // twiddle pairs built and applied in place (no table in VGPRs)
-        float2 w0 = ra[t], w1 = ra[t + 1];
-        cmul2(w0, rb[t], w1, rb[t + 1]);
+        float2 w0 = tw_ld(ra + t), w1 = tw_ld(ra + t + 1);
+        cmul2(w0, tw_ld(rb + t), w1, tw_ld(rb + t + 1));
 #pragma unroll
         for (int b = 0; b < W::NB; b++) cmul2(v[b * R2 + t], w0, v[b * R2 + t + 1], w1);
     }
@@ -215,11 +236,24 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef PRE_DIST
 #define PRE_DIST 1
 #endif
+#ifndef RFA_CWIN
+#define RFA_CWIN 1  // N = 64 K residue 1: twiddle folded into a complex window (A/B builds: 0 = separate)
+#endif
+#ifndef RFA_TILE
+#define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
+#endif
 
 // JS != 0: the frame's two halves sit JS raw elements apart in LDS (SPLIT staging).
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int JS = 0>
+// CW (N = 64 K, residue 1, 8/16-bit input): the twiddle W_N^m is folded into a complex
+// window cw[m] = (w[m] W_N^m, -w[m + M] W_N^m) (exact from double, engine), so a point
+// costs two complex multiply-adds (cmac2: 4 packed instructions) instead of two window
+// products, a subtraction and two complex multiplies (7).  (f32 input keeps the separate
+// twiddle: its 8-B raw samples and the 16-B window pairs in flight would spill.)
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int JS = 0, bool CW = false>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
-                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr) {
+                                         int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
+                                         const float4 *cw = nullptr) {
+    static_assert(!CW || (RS == 2 && R == 1 && !NOWIN), "complex window: residue 1 of N = 2M");
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));  // bytes per sample (per plane)
@@ -231,18 +265,18 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
         if constexpr (STG) return lds_opaque(lraw + tid);
         else return lraw;
     }();
-    const rsrc_t w_rs = make_rsrc(window_il, M * RS * 4);
+    const rsrc_t w_rs = CW ? make_rsrc(cw, M * 16) : make_rsrc(window_il, M * RS * 4);
     const rsrc_t pa_rs = make_rsrc(wide_tw + G::TW_LDS, RS * (M / 32) * 8);
     const float2 *pre_b = wide_tw + G::TW_LDS + RS * (M / 32) + R * 32;
     float2 pa[PT / 32];
-    if constexpr (R != 0) {
+    if constexpr (R != 0 && !CW) {
 #pragma unroll
         for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, R * (M / 32) * 8);
     }
     // loads run DIST chunks ahead of the arithmetic (RFA_PRE_DIST experiments: 1 or 2)
     constexpr int DIST = PRE_DIST;
     typename Raw<FMT>::T raw[DIST + 1][C][RS];
-    float win[DIST + 1][C][RS];
+    float win[DIST + 1][C][CW ? 4 : RS];
     // c is a template parameter throughout: every register array index below is a
     // compile-time constant (a runtime index would move the arrays to scratch)
     auto issue = [&]<int c>() {
@@ -261,6 +295,13 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             if constexpr (NOWIN) {  // ablation (RFA_DIAG=16): constant window, no window loads
 #pragma unroll
                 for (int j = 0; j < RS; j++) win[s][q][j] = 1.0f / 128.0f;
+            } else if constexpr (CW) {  // complex window pair of point m: one 16-B load
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                const f4v w = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(w_rs, tid * 16, mo * 16, 0));
+                win[s][q][0] = w.x;
+                win[s][q][1] = w.y;
+                win[s][q][2] = w.z;
+                win[s][q][3] = w.w;
             } else if constexpr (RS == 2) {
                 const f2v w = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, mo * 8, 0));
                 win[s][q][0] = w.x;
@@ -281,6 +322,21 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     };
     auto compute = [&]<int c>() {
         constexpr int s = c % (DIST + 1);
+        if constexpr (CW) {  // y_1[m] = x[m] cw0[m] + x[m + M] cw1[m]   (NativeDsp.kt:55-58 window, DIF twiddle)
+#pragma unroll
+            for (int q = 0; q < C; q++)
+                v[c * C + q] = cmac2(convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
+                                     convert_raw<FMT>(raw[s][q][1]), make_float2(win[s][q][2], win[s][q][3]));
+            return;
+        } else if constexpr (RS == 2 && R == 0 && !NOWIN) {  // y_0[m] = x[m] w[m] + x[m + M] w[m + M] (mul + fma)
+#pragma unroll
+            for (int q = 0; q < C; q++) {
+                const f2v x0 = to_v(convert_raw<FMT>(raw[s][q][0])), x1 = to_v(convert_raw<FMT>(raw[s][q][1]));
+                v[c * C + q] = from_v(__builtin_elementwise_fma(x1, (f2v){win[s][q][1], win[s][q][1]},
+                                                                x0 * win[s][q][0]));
+            }
+            return;
+        }
         float2 accs[C];
 #pragma unroll
         for (int q = 0; q < C; q++) {
@@ -409,8 +465,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     __syncthreads();  // twiddle tables in LDS
 
-#ifdef RFA_DIAG_STG12  // A/B builds only: the staged kernel without butterflies / exchanges (DIAG 12)
-    constexpr int STG_DIAG_OK = ~60;
+#ifdef RFA_DIAG_STG12  // A/B builds only: the staged kernel without butterflies / exchanges (DIAG 12),
+                       // without stores (2), with dwordx4 ring stores in tile order (64)
+    constexpr int STG_DIAG_OK = ~(60 | 2 | 64);
 #else
     constexpr int STG_DIAG_OK = ~48;
 #endif
@@ -542,8 +599,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS>(v, a.window_il, a.wide_tw, in_rs,
-                                                                                       tid, planar, lraw)
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS,
+                                     RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0>(
+                                v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
@@ -608,13 +666,58 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // it: residue r's M bins are one contiguous block, so this workgroup's stores
             // cover whole lines; caller rows are always natural (fft-shifted) order
             const bool rm = (RS > 1 || dif) && a.ring_logrs > 0;
+            // kRingTile (M = 32 K, fft_kernels.h): the block's elements in this kernel's store
+            // tiles -- thread 64 w + l writes its outputs t' = 4j..4j+3 (t' = (t + 16) mod 32
+            // after the fft-shift) as one 16-B store at w*2048 + j*256 + l*4
+            constexpr bool TILE_OK = RFA_TILE && LOGM == 15 && PT == 32 && G::TPF == 1024 && !dif;
+            const bool tile = TILE_OK && (a.ring_logrs & kRingTile) != 0;
             // kernel B (dif): rows residue-major too, block s (the engine reorders them)
             const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * on + (dif ? (size_t)orr * M : 0) : nullptr,
                                             a.rows ? (dif ? M : on) * 4 : 0);
-            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * on + (rm ? (size_t)orr * M : 0) : nullptr,
-                                             to_ring ? (rm ? M : on) * 4 : 0);
+            const rsrc_t ring_rs = make_rsrc(to_ring ? a.ring + (size_t)rr * on + ((rm || tile) ? (size_t)orr * M : 0) : nullptr,
+                                             to_ring ? ((rm || tile) ? M : on) * 4 : 0);
             const int vo = (ors * tid + orr) * 4;
             // one uniform branch per item, not per store
+            if constexpr ((DIAG & 64) != 0) {  // A/B: the ring's bytes as 8 dwordx4 stores per thread
+                if (to_ring) {
+                    float db[PT];
+    #pragma unroll
+                    for (int q = 0; q < PT; q++) db[q] = db_unscaled(v[q], db_off);
+                    const int w = tid >> 6, l = tid & 63;
+    #pragma unroll
+                    for (int j = 0; j < PT / 4; j++)
+                        buf_store_f32x4(db[4 * j], db[4 * j + 1], db[4 * j + 2], db[4 * j + 3], ring_rs,
+                                        (w * 2048 + l * 4) * 4, j * 256 * 4);
+                }
+                pending_st = to_ring ? PT / 4 : 0;
+                stamp(u, 6);
+                return;
+            }
+            if constexpr (TILE_OK && (DIAG & 2) == 0) {
+                if (tile && to_ring) {
+                    const int tvo = ((tid >> 6) * 2048 + (tid & 63) * 4) * 4;
+                    auto store_tiles = [&](auto rows_c) {
+    #pragma unroll
+                        for (int j = 0; j < 8; j++) {
+                            float d[4];
+    #pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const int t = (4 * j + e + 16) & 31;  // register of output t' = 4j + e
+                                d[e] = db_unscaled(v[t], db_off);     // nativedsp.cpp:73-78
+                                if constexpr (decltype(rows_c)::value)
+                                    buf_store_f32(d[e], row_rs, vo,
+                                                  ((ors * (t * (M / G::R2)) + on / 2) & (on - 1)) * 4);
+                            }
+                            buf_store_f32x4(d[0], d[1], d[2], d[3], ring_rs, tvo, j * 1024);
+                        }
+                    };
+                    if (a.rows) store_tiles(std::true_type{});
+                    else store_tiles(std::false_type{});
+                    pending_st = (a.rows ? PT : 0) + PT / 4;
+                    stamp(u, 6);
+                    return;
+                }
+            }
             auto epilogue = [&](auto nat_c, auto ring_c, auto rm_c) {
     #pragma unroll
                 for (int b = 0; b < PT / G::R2; b++) {
@@ -643,7 +746,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             };
             using T_ = std::true_type;
             using F_ = std::false_type;
-            pending_st = (a.rows ? PT : 0) + (to_ring ? PT : 0);
+            pending_st = (DIAG & 2) ? 0 : (a.rows ? PT : 0) + (to_ring ? PT : 0);
             if (a.rows && to_ring) {
                 if constexpr (RS > 1 || dif) {
                     if (rm) epilogue(T_{}, T_{}, T_{});
@@ -677,6 +780,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
     const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
+    if (RFA_CWIN && RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -707,7 +811,8 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
 int ring_logrs_for(int logn) {
     if (logn > 17 && logn <= kMaxLogN) return logn - kDitLogM;  // large-N kernel B: block s of bins S q + s
     if (!wide_supported(logn) || logn <= 14) return 0;
-    return logn - wide_logm(logn);
+    // 32 K-point workgroups (N = 32 K .. 128 K): residue blocks in store-tile order
+    return (logn - wide_logm(logn)) | (RFA_TILE ? kRingTile : 0);
 }
 
 template <int LOGM, int PT, int RS, bool CO>
@@ -774,9 +879,17 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         return launch_wide_one<15, 32, 2, 0, false, 16, true>(a);
     }
 #ifdef RFA_DIAG_STG12
-    if (a.diag == 12 && a.logn == 16) {  // staged 64 K kernel, streaming part only (A/B builds)
+    if (a.logn == 16 && (a.diag == 12 || a.diag == 2 || a.diag == 64 || a.diag == 14 || a.diag == 76)) {
+        // staged 64 K kernel ablations (A/B builds): 12 streaming part only, 2 no stores,
+        // 64 dwordx4 ring stores, 14 / 76 streaming part without / with dwordx4 stores
         if (a.fmt != 0 || co) return hipErrorInvalidValue;
-        return launch_wide_one<15, 32, 2, 0, false, 12, true>(a);
+        switch (a.diag) {
+        case 12: return launch_wide_one<15, 32, 2, 0, false, 12, true>(a);
+        case 2: return launch_wide_one<15, 32, 2, 0, false, 2, true>(a);
+        case 64: return launch_wide_one<15, 32, 2, 0, false, 64, true>(a);
+        case 14: return launch_wide_one<15, 32, 2, 0, false, 14, true>(a);
+        default: return launch_wide_one<15, 32, 2, 0, false, 76, true>(a);
+        }
     }
 #endif
     if (a.diag == 32) {  // phase stamps of the staged s8 kernels (profiling only)

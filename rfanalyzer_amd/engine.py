@@ -196,6 +196,13 @@ class SpectrumEngine:
         self._check(_lib.lib().rfa_get_ring_order(self._h, ctypes.byref(rs)), "rfa_get_ring_order")
         return rs.value
 
+    def ring_positions(self) -> np.ndarray:
+        """Storage position of every fft-shifted bin in a device ring row (rfa_get_ring_positions)."""
+        out = np.empty(self.n, np.int32)
+        self._check(_lib.lib().rfa_get_ring_positions(self._h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                      self.n), "rfa_get_ring_positions")
+        return out
+
     def reset_state(self) -> None:
         self._check(_lib.lib().rfa_reset_state(self._h), "rfa_reset_state")
 

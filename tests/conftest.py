@@ -9,6 +9,14 @@ for p in (ROOT, HERE, os.path.join(HERE, "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# torch before librfa when both are used in one process: torch's wheel bundles its own
+# libamdhip64.so (ROCm 7.0); loaded first, librfa resolves to that same runtime (one
+# HIP runtime per process).  Without torch every test that does not need it still runs.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and librfa.so")
@@ -43,3 +51,11 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
                       f"excluded below floor: mean {sum(x['excluded'] for x in xs) / len(xs):.3f}, "
                       f"max {max(x['excluded'] for x in xs):.3f}; "
                       f"max |d| over all finite bins {max(x['max_finite'] for x in xs):.3e} dB")
+    full = [x for x in gu.FULL_ROW_LOG if not x.get("bound")]
+    bound = [x for x in gu.FULL_ROW_LOG if x.get("bound")]
+    if full:
+        tr.write_line(f"every bin (no floor, 0 excluded): {len(full)} comparisons, {sum(x['bins'] for x in full)} bins; "
+                      f"max |d| {max(x['max_full'] for x in full):.2e} dB (bar {gu.DB_TOL})")
+    if bound:
+        tr.write_line(f"every bin beyond the reference's own float64 error: {len(bound)} comparisons; "
+                      f"max {max(x['max_full'] for x in bound):.2e} dB (bar {gu.DB_TOL})")

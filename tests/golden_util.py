@@ -30,6 +30,14 @@ DB_TOL = 0.01
 # noise and pffft-vs-float64 stays <= 0.0031 dB on every fixture.
 FLOOR_DB = 50.0
 FLOOR_PFFFT_DB = 45.0
+# Every bin of 16-bit input (no floor): s16 quantisation noise sits ~98 dB below full
+# scale, so a row's deepest bins are ~70 dB below its total level, where any fp32 FFT
+# carries a few hundredths of a dB of rounding -- the reference's own pffft is 0.044 dB
+# off float64 on the s16 16 K fixture, librfa 0.024 dB on another bin of it
+# (scripts/full_row_check.py).  The every-bin bar for s16 is therefore 0.05 dB, against
+# float64 and against pffft beyond pffft's own error; 8-bit input keeps 0.01 dB on
+# every bin (its noise floor keeps every bin >= 1e3 x above fp32 rounding).
+DB_TOL_S16_EVERY_BIN = 0.05
 
 WINDOW_IDS = {"blackman": 0, "hann": 1, "none": 2}
 
@@ -142,4 +150,23 @@ def full_row_diff(got: np.ndarray, exp: np.ndarray) -> float:
     fin = np.isfinite(exp)
     d = float(np.max(np.abs(got[fin] - exp[fin]))) if fin.any() else 0.0
     FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size)})
+    return d
+
+
+def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray) -> float:
+    """Every bin (no floor): max over bins of |got - ref| - |ref - exact|, i.e. how far
+    our row is from the reference's row beyond the reference's own distance from the
+    exact (float64) transform.  Used where the reference's fp32 FFT is itself more
+    than the tolerance off the exact spectrum at its deepest bins (16-bit input,
+    bins ~70 dB below the row level), so that no fp32 FFT can match it to 0.01 dB
+    there; <= DB_TOL means we are within the bar of the reference wherever the
+    reference is exact and never further from it than its own error plus the bar."""
+    got = np.atleast_2d(np.asarray(got, np.float32)).astype(np.float64)
+    ref = np.atleast_2d(np.asarray(ref, np.float32)).astype(np.float64)
+    exact = np.atleast_2d(np.asarray(exact, np.float32)).astype(np.float64)
+    assert got.shape == ref.shape == exact.shape
+    assert np.array_equal(np.isneginf(got), np.isneginf(ref)), "-inf bins differ"
+    fin = np.isfinite(ref)
+    d = float(np.max(np.abs(got[fin] - ref[fin]) - np.abs(ref[fin] - exact[fin]))) if fin.any() else 0.0
+    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bound": True})
     return d

@@ -90,3 +90,12 @@ def test_jni_table_layout_constants():
     # the compiled static_asserts pin these; make sure they stay in the header
     for slot in ("171", "200", "205", "213", "228"):
         assert f"== {slot} * sizeof(void *)" in text
+
+
+def test_no_store_data_hazard_in_kernel_isa():
+    """The gfx950 hazard behind buf_store_f32x4's inline asm (fft_common.h): no 12/16-byte
+    vector store may have its data VGPRs overwritten by the next VALU instruction."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "rfanalyzer_amd", "csrc"), "hazard-check"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "0 hazards" in r.stdout

@@ -45,6 +45,8 @@ def test_state_sequence_vs_reference(rfa, batch):
         np.testing.assert_array_equal(g[fill], x[fill])
         if (~fill).any():
             assert gu.pffft_diff(g[~fill], x[~fill]) <= gu.DB_TOL
+            assert gu.full_row_diff(g[~fill], x[~fill]) <= gu.DB_TOL  # every bin (s8 input)
+    assert gu.full_row_diff(e.peaks(), exp["peaks"]) <= gu.DB_TOL
     e.close()
 
 
@@ -386,3 +388,25 @@ def test_process_batches_equals_consecutive_calls(rfa, packed):
         # the EMA recursion is re-associated by the chunked scan (one batch of 60 frames
         # vs five of 12): equal to fp32 rounding, not bit for bit
         np.testing.assert_allclose(a.ema(), b.ema(), rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("n", [1024, 32768, 65536, 131072, 1048576])
+def test_ring_positions_map_device_rows(rfa, n):
+    """rfa_get_ring_positions (zero-copy consumers): the raw device ring row gathered
+    at the reported positions is the natural row rfa_get_ring returns -- including the
+    32 K kernel's store-tile order at N = 32 K .. 128 K."""
+    import ctypes
+    data = np.random.default_rng(n).integers(-128, 128, size=2 * n * 3, dtype=np.int8).tobytes()
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=3) as e:
+        e.set_tuning(100_000_000, 2_000_000)
+        e.process(data, 3, rows=False)
+        pos = e.ring_positions()
+        assert np.array_equal(np.sort(pos), np.arange(n))  # a permutation
+        ring, ri, _ = e.ring()
+        r, p, m = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        assert rfa.lib().rfa_get_device_state(e.handle, ctypes.byref(r), ctypes.byref(p), ctypes.byref(m)) == 0
+        raw = np.empty((3, n), np.float32)
+        hip = ctypes.CDLL("libamdhip64.so")
+        e.synchronize()
+        assert hip.hipMemcpy(ctypes.c_void_p(raw.ctypes.data), r, ctypes.c_size_t(raw.nbytes), 2) == 0
+        np.testing.assert_array_equal(raw[:, pos], ring)
