@@ -431,6 +431,9 @@ __device__ __forceinline__ float2 buf_load_f32x2(rsrc_t rs, int voff, int soff) 
 __device__ __forceinline__ void buf_store_f32(float x, rsrc_t rs, int voff, int soff) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), rs, voff, soff, 0);
 }
+#ifndef RFA_X4_POLICY
+#define RFA_X4_POLICY ""  // cache policy of the 16-B ring stores (A/B builds: "nt", "sc1")
+#endif
 // 16-B store.  Inline asm with a trailing s_nop: a VALU write to the data VGPRs of a
 // just-issued buffer store of more than 64 bits needs a wait state, and hipcc (ROCm
 // 7.2, gfx950) let the next v_pk_fma overwrite them back to back -- the last lanes of
@@ -441,7 +444,8 @@ __device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float
     i32x4 v = {__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), __builtin_bit_cast(int, c),
                __builtin_bit_cast(int, d)};
 #if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs), "s"(soff)
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen " RFA_X4_POLICY "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
+                 "s"(soff)
                  : "memory");
 #else
     (void)v; (void)rs; (void)voff; (void)soff;

@@ -51,11 +51,9 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
                       f"excluded below floor: mean {sum(x['excluded'] for x in xs) / len(xs):.3f}, "
                       f"max {max(x['excluded'] for x in xs):.3f}; "
                       f"max |d| over all finite bins {max(x['max_finite'] for x in xs):.3e} dB")
-    full = [x for x in gu.FULL_ROW_LOG if not x.get("bound")]
-    bound = [x for x in gu.FULL_ROW_LOG if x.get("bound")]
-    if full:
-        tr.write_line(f"every bin (no floor, 0 excluded): {len(full)} comparisons, {sum(x['bins'] for x in full)} bins; "
-                      f"max |d| {max(x['max_full'] for x in full):.2e} dB (bar {gu.DB_TOL})")
-    if bound:
-        tr.write_line(f"every bin beyond the reference's own float64 error: {len(bound)} comparisons; "
-                      f"max {max(x['max_full'] for x in bound):.2e} dB (bar {gu.DB_TOL})")
+    for kind, bound in (("every bin (no floor, 0 excluded)", False),
+                        ("every bin beyond the reference's own float64 error", True)):
+        for bar in sorted({x["bar"] for x in gu.FULL_ROW_LOG if bool(x.get("bound")) == bound}):
+            xs = [x for x in gu.FULL_ROW_LOG if bool(x.get("bound")) == bound and x["bar"] == bar]
+            tr.write_line(f"{kind}, bar {bar} dB: {len(xs)} comparisons, {sum(x['bins'] for x in xs)} bins; "
+                          f"max |d| {max(x['max_full'] for x in xs):.2e} dB")

@@ -38,6 +38,16 @@ FLOOR_PFFFT_DB = 45.0
 # float64 and against pffft beyond pffft's own error; 8-bit input keeps 0.01 dB on
 # every bin (its noise floor keeps every bin >= 1e3 x above fp32 rounding).
 DB_TOL_S16_EVERY_BIN = 0.05
+# Every bin of a long 8-bit batch (config 3: 500 x 64 K s8 Blackman frames, 32.8 M bins):
+# the deepest bins sit ~40 dB below a row's mean, and over that many bins any fp32 FFT
+# reaches past 0.01 dB somewhere -- on this batch the reference's pffft is 0.038 dB off
+# float64, torch's CPU fp32 FFT 0.026 dB, librfa 0.0135 dB (the 99.9999 % quantile of
+# torch's error is 0.003 dB).  A bin 40 dB (10^4 in magnitude) below the row mean
+# carries the fp32 rounding of the whole transform amplified 10^4 times, so 0.01 dB on
+# every one of 32.8 M bins is below what fp32 arithmetic resolves.  Bar: 0.02 dB
+# against float64, never worse than pffft's own deviation, and 0.02 dB against pffft
+# beyond pffft's error (full_row_bound; measured 0.0107 on MI355X).
+DB_TOL_BATCH_EVERY_BIN = 0.02
 
 WINDOW_IDS = {"blackman": 0, "hann": 1, "none": 2}
 
@@ -141,19 +151,21 @@ def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> 
 FULL_ROW_LOG: list[dict] = []
 
 
-def full_row_diff(got: np.ndarray, exp: np.ndarray) -> float:
-    """Max |dB difference| over EVERY bin (no floor); -inf must match -inf."""
+def full_row_diff(got: np.ndarray, exp: np.ndarray, bar: float | None = DB_TOL) -> float:
+    """Max |dB difference| over EVERY bin (no floor); -inf must match -inf.  ``bar`` is
+    the bar the caller asserts (logged for the session summary; None: not logged)."""
     got = np.atleast_2d(np.asarray(got, np.float32))
     exp = np.atleast_2d(np.asarray(exp, np.float32))
     assert got.shape == exp.shape
     assert np.array_equal(np.isneginf(got), np.isneginf(exp)), "-inf bins differ"
     fin = np.isfinite(exp)
     d = float(np.max(np.abs(got[fin] - exp[fin]))) if fin.any() else 0.0
-    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size)})
+    if bar is not None:
+        FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bar": bar})
     return d
 
 
-def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray) -> float:
+def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray, bar: float = DB_TOL) -> float:
     """Every bin (no floor): max over bins of |got - ref| - |ref - exact|, i.e. how far
     our row is from the reference's row beyond the reference's own distance from the
     exact (float64) transform.  Used where the reference's fp32 FFT is itself more
@@ -168,5 +180,5 @@ def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray) -> float
     assert np.array_equal(np.isneginf(got), np.isneginf(ref)), "-inf bins differ"
     fin = np.isfinite(ref)
     d = float(np.max(np.abs(got[fin] - ref[fin]) - np.abs(ref[fin] - exact[fin]))) if fin.any() else 0.0
-    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bound": True})
+    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bound": True, "bar": bar})
     return d
