@@ -31,7 +31,6 @@ struct rfa_handle {
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     float *d_window = nullptr;
-    int window_sym = 0;               // d_window symmetric (w[n] == w[N-1-n])
     float *d_window_none = nullptr;   // all ones (already-windowed f32 seams)
     float *d_window_black = nullptr;  // unscaled Blackman (NativeDsp.kt seam, f32 planar)
     float *d_window_il = nullptr;     // N > 32768: scaled window as [m][j], m < 32768, j < N/32768
@@ -291,7 +290,6 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     if (a.window == h->d_window) {
         a.window_il = h->d_window_il;
         a.window_cw = h->d_window_cw;
-        a.window_sym = h->window_sym;
     }
     else if (h->logn > 14) a.variant = 1;  // seam windows have no interleaved copy: narrow kernel
     // the ring order is a property of the wide kernel's residue split (ring_pos)
@@ -439,10 +437,6 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
                         : cfg->input_format == RFA_IN_S16LE                                ? 1.0f / 32768.0f
                                                                                            : 1.0f;
     for (float &x : w) x *= scale;
-    // w[n] == w[N-1-n] bit for bit (the wide 64 K kernel's mirrored lanes rely on it)
-    h->window_sym = 1;
-    for (int i = 0; i < n / 2; i++)
-        if (w[i] != w[(size_t)n - 1 - i]) h->window_sym = 0;
     float **tabs[3] = {&h->d_window, &h->d_window_none, &h->d_window_black};
     const float *src[3] = {w.data(), ones.data(), black.data()};
     for (int i = 0; i < 3; i++) {

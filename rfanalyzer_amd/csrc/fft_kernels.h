@@ -62,9 +62,6 @@ struct FftLaunch {
     // N = 64 K, residue 1 of the pre-stage: the twiddle folded into a complex window,
     // [m] = (w[m] W_N^m, -w[m + M] W_N^m) as float4, m < M (null: separate twiddle)
     const float4 *window_cw = nullptr;
-    // window[n] == window[N-1-n] for every n (engine check; Blackman / Hann / none are, bit
-    // for bit): the 64 K staged kernel then reads each window value once per work item
-    int window_sym = 0;
     // wide kernel twiddle blob (exact, from double): pass-1 [32][R1] | pass-2 A,B [16][16] |
     // pre-stage pre_a [RS][512] | pre_b [RS][32]   (DESIGN.md "Twiddles")
     const float2 *wide_tw = nullptr;  // wide_twiddles() blob (layout in fft_wide.hip WGeo)

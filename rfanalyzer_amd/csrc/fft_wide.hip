@@ -155,49 +155,6 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     }
 }
 
-// Mirrored lanes (MIR, the 64 K staged kernel with a symmetric window): lanes i and
-// 15 - i of each 16-lane row hold the logical threads tl and 1023 - tl of the pre-stage
-// and pass 0 (lane_tl below), so a point's second window value is the partner lane's
-// own (prestage_mir).  Exchange 0 then runs in four rounds by 128-thread blocks
-// q = tl >> 7 paired with 7 - q (the partner's block): part(q) depends only on
-// q ^ (q >> 1) bits that are the same for q and 7 - q, so a wave's 64 lanes share their
-// part and every round is written by four whole waves, as in exchange<0, ..., 4>.
-// The two blocks of a part sit at [0, 4096) and [4096, 8192) of region A.  Readers
-// keep the hardware thread index (pass-1 layout): input t' of thread tid is position
-// tid + 1024 t', block t' >> 2 -- a compile-time round per register.
-__device__ __forceinline__ int lane_tl(int h) {
-    const int w = h >> 6, row = (h >> 4) & 3, i = h & 15;
-    const int base = 32 * w + 8 * row;
-    return i < 8 ? base + i : 1023 - (base + 15 - i);
-}
-__host__ __device__ constexpr int mir_part(int q) { return (((q >> 1) ^ (q >> 2)) & 1) << 1 | ((q ^ (q >> 1)) & 1); }
-
-template <int LOGM, int PT>
-__device__ __forceinline__ void exchange0_mir(float2 (&v)[PT], float2 *buf, int tl, int tid) {
-    using G = WGeo<LOGM, PT>;
-    static_assert(LOGM == 15 && PT == 32 && G::TPF == 1024, "64 K staged kernel: 32 K points, 1024 threads");
-    constexpr int QB = 4096;  // positions of one 128-thread block
-    const int q = tl >> 7;
-    const int my_part = mir_part(q);  // wave-uniform
-    const int wbase = padw(32 * (tl & 127) + QB * (q >> 2));
-    const int rbase = padw(tid);
-    float2 nv[32];
-#pragma unroll
-    for (int h = 0; h < 4; h++) {
-        if (my_part == h) {
-#pragma unroll
-            for (int t = 0; t < 32; t++) buf[wbase + padw(t)] = v[t];
-        }
-        lds_barrier();
-#pragma unroll
-        for (int t = 0; t < 32; t++)
-            if (mir_part(t >> 2) == h) nv[t] = buf[rbase + padw(1024 * (t & 3) + QB * (t >> 4))];
-        lds_barrier();
-    }
-#pragma unroll
-    for (int t = 0; t < 32; t++) v[t] = nv[t];
-}
-
 // Pass 1: k = tid & 31 is the same for every butterfly of the thread; its
 // twiddles W_{32 R}^{t k} sit contiguously at twp1[k][t-1] (exact, from double).
 template <int LOGM, int PT>
@@ -282,9 +239,6 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #endif
 #ifndef RFA_CWIN
 #define RFA_CWIN 1  // N = 64 K residue 1: twiddle folded into a complex window (A/B builds: 0 = separate)
-#endif
-#ifndef RFA_MIRROR
-#define RFA_MIRROR 0  // A/B only: mirrored lanes (profiles/r03/mirror_lanes_ab.txt: -2 %, coherent twiddle error)
 #endif
 #ifndef RFA_TILE
 #define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
@@ -445,70 +399,6 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     }(std::make_integer_sequence<int, NCH>{});
 }
 
-// MIR pre-stage (N = 64 K, 8-bit input staged in LDS, symmetric window): logical
-// thread tl (lane_tl), point m = tl + 1024 t.  w[m] is this lane's own load from the
-// natural window's first half; w[m + M] = w[M - 1 - m] (symmetry) is the partner lane's
-// w[m'] of point 31 - t, one row_mirror DPP move away -- 4 B of window per point
-// instead of the interleaved pair's 8 or the complex window's 16.  Chunk c holds the
-// points t = 2c, 2c+1, 31-2c, 30-2c, so a chunk's partner values are its own.
-//   y_0[m] = x[m] w[m] + x[m + M] w[m + M]
-//   y_1[m] = (x[m] w[m] - x[m + M] w[m + M]) W_N^m,  W_N^m = pre_a[tl] W_64^t
-template <int LOGM, int PT, int FMT, int R, int JS>
-__device__ __forceinline__ void prestage_mir(float2 (&v)[PT], const float *window, const float2 *wide_tw, int tl,
-                                             const typename Raw<FMT>::T *lraw) {
-    using G = WGeo<LOGM, PT>;
-    constexpr int M = G::M;
-    static_assert(LOGM == 15 && PT == 32 && G::TPF == 1024 && JS != 0, "64 K staged kernel");
-    const auto lr = lds_opaque(lraw + tl);
-    const rsrc_t w_rs = make_rsrc(window, M * 4);
-    float2 pa = make_float2(1.0f, 0.0f);
-    if constexpr (R != 0) pa = buf_load_f32x2(make_rsrc(wide_tw + G::TW_LDS, 2 * (M / 32) * 8), tl * 8, R * (M / 32) * 8);
-    typename Raw<FMT>::T raw[2][4][2];
-    float win[2][4];
-    auto tsel = [](int c, int q) constexpr { return q < 2 ? 2 * c + q : 31 - 2 * c - (q - 2); };
-    auto issue = [&]<int c>() {
-        constexpr int s = c & 1;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int t = tsel(c, q);
-            raw[s][q][0] = lr[1024 * t];
-            raw[s][q][1] = lr[1024 * t + JS];
-            win[s][q] = buf_load_f32(w_rs, tl * 4, 1024 * t * 4);
-        }
-    };
-    auto compute = [&]<int c>() {
-        constexpr int s = c & 1;
-        [&]<int... Qs>(std::integer_sequence<int, Qs...>) {
-            (
-                [&] {
-                    constexpr int q = Qs, t = tsel(c, Qs);
-                    // row_mirror (DPP 0x140): lane i reads lane 15 - i of its row
-                    const float w1 = __builtin_bit_cast(
-                        float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, win[s][q ^ 2]), 0x140, 0xf, 0xf, true));
-                    const f2v x0 = to_v(convert_raw<FMT>(raw[s][q][0])), x1 = to_v(convert_raw<FMT>(raw[s][q][1]));
-                    if constexpr (R == 0) {
-                        v[t] = from_v(__builtin_elementwise_fma(x1, (f2v){w1, w1}, x0 * win[s][q]));
-                    } else {
-                        const float2 d = from_v(__builtin_elementwise_fma(-x1, (f2v){w1, w1}, x0 * win[s][q]));
-                        v[t] = w64<(t * R) & 63>(cmul(d, pa));
-                    }
-                }(),
-                ...);
-        }(std::make_integer_sequence<int, 4>{});
-    };
-    issue.template operator()<0>();
-    [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
-        (
-            [&] {
-                if constexpr (Cs + 1 < 8) issue.template operator()<Cs + 1>();
-                __builtin_amdgcn_sched_barrier(0);
-                compute.template operator()<Cs>();
-                __builtin_amdgcn_sched_barrier(0);
-            }(),
-            ...);
-    }(std::make_integer_sequence<int, 8>{});
-}
-
 // LDS-DMA staging of one frame's raw bytes (STG kernels): the frame's n*BPS
 // bytes go HBM -> LDS exchange buffer in natural order, 1 KiB per wave
 // instruction (buffer_load_dwordx4 ... lds: no VGPRs, 16 B per lane), issued
@@ -549,7 +439,7 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
 // STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
 // formats, one sub-FFT per workgroup, frame fits the exchange buffer; the
 // host launches a persistent grid and checks 16-byte alignment).
-template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false, bool MIR = false>
+template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false>
 __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) fft_wide_kernel(FftLaunch a) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
@@ -592,9 +482,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
-    static_assert(!MIR || (SPLIT && (DIAG & 16) == 0), "mirrored lanes: the 64 K split-staged kernel");
-    // MIR: logical thread of the pre-stage, pass 0 and exchange 0's writes (lane_tl)
-    const int tl = MIR ? lane_tl(threadIdx.x) : tid;
     static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
@@ -649,10 +536,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         int z;
         asm volatile("s_mov_b32 %0, 0" : "=s"(z));
         const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
-        // MIR: the logical thread, opaque per item (bases derived from it are rebuilt
-        // inside the item instead of hoisted out of the loop and spilled)
-        int tli = tl;
-        if constexpr (MIR) asm volatile("" : "+v"(tli));
         int frame, r;
         int dif_r = 0;  // large-N kernel B: column residue s of the frame (bins S q + s)
         if constexpr (RS == 1) {
@@ -716,17 +599,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // residue r is wave-uniform: instantiate the pre-stage per r so the
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
-            if constexpr (MIR) {
-                if (r == 0) prestage_mir<LOGM, PT, FMT, 0, JS>(v, a.window, a.wide_tw, tli, lraw);
-                else prestage_mir<LOGM, PT, FMT, 1, JS>(v, a.window, a.wide_tw, tli, lraw);
-            } else {
-                [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                    ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS,
-                                         RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0>(
-                                    v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
-                              : void()), ...);
-                }(std::make_integer_sequence<int, RS>{});
-            }
+            [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS,
+                                     RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0>(
+                                v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
+                          : void()), ...);
+            }(std::make_integer_sequence<int, RS>{});
         }
 
         // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
@@ -742,8 +620,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
         }
-        if constexpr (MIR) exchange0_mir<LOGM, PT>(v, buf, tli, tid);
-        else if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
         if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
@@ -899,15 +776,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     }
 }
 
-template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false, bool MIR = false>
+template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false>
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
-    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG, MIR>;
+    auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
     const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
-    if (RFA_CWIN && RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !MIR && !a.window_cw)
-        return hipErrorInvalidValue;                      // residue 1's table
-    if (MIR && !a.window_sym) return hipErrorInvalidValue;  // the partner lane's value is w[m + M]
+    if (RFA_CWIN && RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -957,10 +832,6 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         constexpr bool stg8 = G::SLOTS == 1 && M * RS * 2 <= G::HALFP * 8;
         constexpr bool stg16 = G::SLOTS == 1 && M * RS * 4 <= G::HALFP * 8;
         if constexpr (stg8) {
-            // 64 K split-staged kernel, symmetric window: mirrored lanes (one window load per point)
-            constexpr bool mir_ok = RFA_MIRROR && LOGM == 15 && RS == 2 && PT == 32;
-            if (mir_ok && stg && a.window_sym && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true, mir_ok>(a);
-            if (mir_ok && stg && a.window_sym && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true, mir_ok>(a);
             if (stg && a.fmt == 0) return launch_wide_one<LOGM, PT, RS, 0, false, 0, true>(a);
             if (stg && a.fmt == 1) return launch_wide_one<LOGM, PT, RS, 1, false, 0, true>(a);
         }
@@ -1036,9 +907,7 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         case 13: return launch_wide_one<13, 32, 1, 0, false, 32, true>(a);
         case 14: return launch_wide_one<14, 32, 1, 0, false, 32, true>(a);
         case 15: return launch_wide_one<15, 32, 1, 0, false, 32, true>(a);
-        case 16:
-            if (RFA_MIRROR && a.window_sym) return launch_wide_one<15, 32, 2, 0, false, 32, true, RFA_MIRROR != 0>(a);
-            return launch_wide_one<15, 32, 2, 0, false, 32, true>(a);
+        case 16: return launch_wide_one<15, 32, 2, 0, false, 32, true>(a);
         default: return hipErrorInvalidValue;
         }
     }

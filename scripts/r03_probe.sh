@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 TAG=${1:-e}
 L=alt/librfa_diag.so
 K="--sizes 65536 --formats s8 --samples 32768000 --state"
-for d in ${STAMPS:-}; do
+for d in ${STAMPS:-0 16}; do
   rm -f gpurun_out/stamps_${TAG}_$d.bin
   RFA_LIB=$L RFA_DIAG=$d RFA_STAMPS_FILE=gpurun_out/stamps_${TAG}_$d.bin timeout -k 10 120 python -u scripts/kbench.py \
     $K --iters 8 > /dev/null 2>&1
