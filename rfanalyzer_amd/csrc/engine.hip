@@ -51,6 +51,7 @@ struct rfa_handle {
     std::string stamps_file;          // RFA_STAMPS_FILE: phase stamps appended per launch
     unsigned long long *d_stamps = nullptr;
     int diag = 0;                     // RFA_DIAG ablation variant
+    int phase_ticks = 0;              // RFA_PHASE_NS (A/B builds)
     int ring_logrs = 0;               // ring row order (fft_kernels.h ring_pos): residue split of the main kernel
     float2 *d_twc = nullptr, *d_twf = nullptr;
     int tw_shift = 0;
@@ -280,6 +281,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
     a.tw_fine = h->d_twf;
     a.tw_shift = h->tw_shift;
     a.diag = h->diag;
+    a.phase_ticks = h->phase_ticks;
     a.stage = h->stage;
     if (h->d_stamps) {
         a.diag |= 32;  // phase stamps (+ RFA_DIAG 16: without window loads)
@@ -491,6 +493,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     // A/B and profiling builds only (scripts/build_variant.sh): ablation switches
     if (const char *d = std::getenv("RFA_KERNEL")) h->variant = std::string(d) == "narrow" ? 1 : 0;
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
+    if (const char *d = std::getenv("RFA_PHASE_NS")) h->phase_ticks = std::atoi(d) / 10;
     if (const char *d = std::getenv("RFA_DIF_PIPE")) h->dif_pipe = std::max(0, std::atoi(d));
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {

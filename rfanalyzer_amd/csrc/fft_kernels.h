@@ -88,6 +88,9 @@ struct FftLaunch {
     // passes, 32 phase stamps); always 0 in the product library
     int diag = 0;
     unsigned long long *stamps = nullptr;  // diag 32: [blocks][16][8] s_memrealtime phase stamps
+    int phase_ticks = 0;  // A/B builds (RFA_PHASE_NS): persistent workgroups of the second half of
+                          // the grid start this many 10-ns ticks late (phase offset between the
+                          // two workgroups of a CU)
     hipStream_t stream = nullptr;
 };
 

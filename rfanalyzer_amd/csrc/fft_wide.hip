@@ -517,6 +517,12 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // followed by a barrier before anyone leaves the FFT.
     // DIAG & 32 (profiling only): s_memrealtime stamps of each item's phases by
     // thread 0 into a.stamps[block][item < 16][8] (engine: RFA_STAMPS_FILE)
+#ifdef RFA_AB_BUILD
+    if (STG && a.phase_ticks > 0 && blockIdx.x >= gridDim.x / 2) {  // A/B: phase offset (RFA_PHASE_NS)
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)a.phase_ticks) __builtin_amdgcn_s_sleep(2);
+    }
+#endif
     int it_count = 0;  // items this workgroup has started (stamps)
     auto stamp = [&](int u, int k) {
         if constexpr ((DIAG & 32) != 0) {
