@@ -736,9 +736,13 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         }
         if (need_state) HIPCHK(h, rfa::launch_state(s));
         if (need_chan) {
-            int rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, n_frames * sizeof(float));
+            // means, then (channels wider than 16384 bins) the per-span partial sums
+            const int spans = rfa::channel_mean_spans(chan_last - chan_first);
+            const size_t words = n_frames * (size_t)(spans > 1 ? 1 + spans : 1);
+            int rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, words * sizeof(float));
             if (rc) return rc;
-            HIPCHK(h, rfa::launch_channel_mean(s, chan_first, chan_last, h->d_chan));
+            HIPCHK(h, rfa::launch_channel_mean(s, chan_first, chan_last, h->d_chan,
+                                               spans > 1 ? h->d_chan + n_frames : nullptr));
             h->chan_count = n_frames;
         }
     }

@@ -155,7 +155,10 @@ struct StateLaunch {
 };
 hipError_t launch_state(const StateLaunch &a);
 // Mean of row[first, last) for every frame (rows addressed as in StateLaunch).
-hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out);
+// channel mean of every frame (FftProcessor.kt:143-157); channels wider than 16384 bins are
+// summed in channel_mean_spans() pieces whose sums go to partial[n_frames][spans] first
+int channel_mean_spans(int width);
+hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out, float *partial);
 
 // Display preprocessing (AnalyzerSurface.kt:599-743), display.hip.  Scalars are
 // computed on the host exactly as the reference does (double / fp32 / Kotlin toInt).

@@ -632,25 +632,65 @@ hipError_t launch_state(const StateLaunch &a) {
     return hipGetLastError();
 }
 
-// FftProcessor.kt:143-157: mean of the channel's dB bins, one lane per frame.  The
-// sum runs sequentially in fp32 in bin order like the reference loop (:150-152),
-// so a frame's mean is bit-exact with that loop over the same row; its latency is
-// one dependent add per bin (channels are narrow: 838 bins for 200 kHz at 1 M /
-// 250 Msps), the bins' loads are independent and pipelined.
-__global__ void __launch_bounds__(64) channel_mean_kernel(StateLaunch a, int first, int last, float *out) {
-    const int f = blockIdx.x * 64 + threadIdx.x;
-    if (f >= a.n_frames) return;
+// FftProcessor.kt:143-157: mean of the channel's dB bins per frame (the squelch input).
+// One workgroup per frame: thread t adds bins first + t, first + t + 256, ... in that
+// order (each wave instruction reads 64 consecutive natural bins of the row), then the
+// 256 partial sums are folded in a fixed tree.  Deterministic, and within a few fp32
+// ulps of the reference's sequential fp32 loop (:150-152) -- which is itself only one
+// rounding order of the sum; the rows it averages already differ from pffft's by up to
+// the FFT tolerance.  Round 2 kept that loop's order exactly, one lane per frame: a
+// dependent add per bin behind a load that gathers 64 rows per wave instruction,
+// +64 us per 500-frame 64 K step for a 1000-bin channel and +2.1 ms for 32000 bins
+// (profiles/r03/channel_mean_ab.txt).
+__global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int first, int last, int span, float *out,
+                                                          float *partial) {
+    __shared__ float part[256];
+    const int f = blockIdx.x, t = threadIdx.x;
     const float *row = state_row(a, f);
     const int lr = state_logrs(a), lm = ring_logm(lr, ilog2_dev(a.n));
+    // wide channels: blockIdx.y takes bins [lo, hi) of the channel (span bins each)
+    const int lo = first + blockIdx.y * span, hi = min(last, lo + span);
     float s = 0.0f;
-#pragma unroll 8
-    for (int i = first; i < last; i++) s += row[ring_pos(i, lr, lm)];
-    out[f] = s / (float)(last - first);
+    int i = lo + t;
+    for (; i + 3 * 256 < hi; i += 4 * 256) {  // four loads in flight per thread
+        const float x0 = row[ring_pos(i, lr, lm)], x1 = row[ring_pos(i + 256, lr, lm)];
+        const float x2 = row[ring_pos(i + 512, lr, lm)], x3 = row[ring_pos(i + 768, lr, lm)];
+        s = (((s + x0) + x1) + x2) + x3;
+    }
+    for (; i < hi; i += 256) s += row[ring_pos(i, lr, lm)];
+    part[t] = s;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h > 0; h >>= 1) {
+        if (t < h) part[t] = part[t] + part[t + h];
+        __syncthreads();
+    }
+    if (t == 0) {
+        if (gridDim.y == 1) out[f] = part[0] / (float)(last - first);
+        else partial[(size_t)f * gridDim.y + blockIdx.y] = part[0];
+    }
 }
 
-hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out) {
+// wide channels: the per-span sums of a frame folded in span order
+__global__ void channel_mean_fold_kernel(int n_frames, int spans, int width, const float *partial, float *out) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n_frames) return;
+    float s = 0.0f;
+    for (int k = 0; k < spans; k++) s += partial[(size_t)f * spans + k];
+    out[f] = s / (float)width;
+}
+
+int channel_mean_spans(int width) { return std::min(64, std::max(1, (width + 16383) / 16384)); }
+
+hipError_t launch_channel_mean(const StateLaunch &a, int first, int last, float *out, float *partial) {
     if (a.n_frames <= 0 || last <= first) return hipSuccess;
-    hipLaunchKernelGGL(channel_mean_kernel, dim3((a.n_frames + 63) / 64), dim3(64), 0, a.stream, a, first, last, out);
+    const int width = last - first, spans = channel_mean_spans(width), span = (width + spans - 1) / spans;
+    if (spans > 1 && !partial) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(channel_mean_kernel, dim3(a.n_frames, spans), dim3(256), 0, a.stream, a, first, last, span, out,
+                       partial);
+    if (spans > 1)
+        hipLaunchKernelGGL(channel_mean_fold_kernel, dim3((a.n_frames + 255) / 256), dim3(256), 0, a.stream, a.n_frames,
+                           spans, width, partial, out);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--state", action="store_true", help="EMA + peak-hold + ring")
     ap.add_argument("--no-prof", action="store_true", help="time steps without the per-launch HIP events")
+    ap.add_argument("--channel-bins", type=int, default=0,
+                    help="with --state: a squelch channel this many bins wide (channel mean per frame)")
     args = ap.parse_args()
     import torch
 
@@ -37,6 +39,10 @@ def main():
             kw = dict(avg="ema", peak_hold=True, ring_rows=max(frames, 300)) if args.state else dict(ring_rows=0)
             with rfanalyzer_amd.SpectrumEngine(n, "blackman", fmt, **kw) as e:
                 e.set_stream(torch.cuda.current_stream().cuda_stream)
+                if args.channel_bins and args.state:  # 1000 Hz per bin: sample rate = 1000 N
+                    f0 = 100_000_000
+                    e.set_tuning(f0, 1000 * n)
+                    e.set_channel(f0 - 500 * args.channel_bins, f0 + 500 * args.channel_bins)
                 out = None if args.state else rows
                 for k in range(3):
                     e.process_tensor(pools[k % 4], frames, 0, out)

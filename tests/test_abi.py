@@ -99,3 +99,12 @@ def test_no_store_data_hazard_in_kernel_isa():
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert "0 hazards" in r.stdout
+
+
+def test_product_library_reads_no_environment(lib):
+    """Determinism: RFA_* switches exist only in A/B builds
+    (-DRFA_AB_BUILD); the product librfa.so does not import getenv at all."""
+    from rfanalyzer_amd import _lib
+    r = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "getenv" not in r.stdout

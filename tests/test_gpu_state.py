@@ -154,6 +154,12 @@ def test_chunked_state_with_silent_frames(rfa, batches):
         assert gu.db_diff(e.ema(), ema_before) <= gu.DB_TOL
 
 
+# channel mean vs the reference's sequential fp32 loop over the same rows: the device
+# folds the bins in a tree; for means around -40 dB over <= 5000 bins the two rounding
+# orders differ by ~1e-5 dB (fp32 ulp of the running sum x sqrt(bins))
+CHAN_SUM_TOL = 2e-4
+
+
 @pytest.mark.parametrize("n,freq,sr,chan", [(4096, 100_000_000, 2_000_000, (100_010_000, 100_060_000)),
                                             (65536, 433_920_000, 20_000_000, (433_000_000, 434_500_000)),
                                             (1048576, 433_920_000, 250_000_000, (400_000_000, 401_000_000)),
@@ -183,9 +189,58 @@ def test_channel_mean_per_frame(rfa, n, freq, sr, chan):
     assert got.size == frames
     np.testing.assert_allclose(got, np.array(exp, np.float32), rtol=0, atol=gu.DB_TOL)
     # the reference's own loop (sequential fp32 sum, :150-152) over the rows the GPU
-    # produced gives the GPU's means bit for bit
+    # produced: the device sums the same bins in a fixed tree order, so the two agree
+    # to fp32 rounding of the sum (CHAN_SUM_TOL), far below the FFT tolerance
     same = [processor.channel_mean(r, n, freq, sr, *chan) for r in gpu_rows]
-    np.testing.assert_array_equal(got, np.array(same, np.float32))
+    np.testing.assert_allclose(got, np.array(same, np.float32), rtol=0, atol=CHAN_SUM_TOL)
+
+
+def test_channel_mean_many_frames_wide_channel(rfa):
+    """channel_mean_kernel on 130 frames and a 1001-bin channel (four strided loads
+    per thread, a tail, the tree fold) read from the ring in store-tile order: equal to
+    the reference's sequential loop over the GPU's own rows to fp32 rounding of the
+    sum, and bit-identical between two runs."""
+    n, frames, freq, sr = 32768, 130, 100_000_000, 32_768_000  # 1000 Hz per bin
+    chan = (freq - 500_500, freq + 500_500)
+    data = signals.frames_bytes(n, frames, "s8", 23, tones=((0.01, 0.3), (-0.2, 0.05)), noise=0.05)
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=frames) as e:
+        e.set_tuning(freq, sr)
+        e.set_channel(*chan)
+        e.process(data, frames, rows=False)
+        ring, _, _ = e.ring()
+        gpu_rows = ring[[(-g) % frames for g in range(frames)]]
+        got = e.channel_means()
+    same = [processor.channel_mean(r, n, freq, sr, *chan) for r in gpu_rows]
+    assert got.size == frames
+    np.testing.assert_allclose(got, np.array(same, np.float32), rtol=0, atol=CHAN_SUM_TOL)
+    # deterministic: the same batch again gives the same means bit for bit
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=frames) as e:
+        e.set_tuning(freq, sr)
+        e.set_channel(*chan)
+        e.process(data, frames, rows=False)
+        np.testing.assert_array_equal(e.channel_means(), got)
+
+
+def test_channel_mean_spans_wide_channel(rfa):
+    """Channels wider than 16384 bins are summed by several workgroups per frame and
+    folded in span order (channel_mean_spans): 40001 bins at 64 K -> three spans.  The
+    sequential fp32 loop's own rounding grows with the bin count, so the comparison is
+    relative (3e-5 of the mean) here; still deterministic bit for bit."""
+    n, frames, freq, sr = 65536, 20, 100_000_000, 65_536_000
+    chan = (freq - 20_000_500, freq + 20_000_500)
+    data = signals.frames_bytes(n, frames, "u8", 29, tones=((0.05, 0.3),), noise=0.05)
+    outs = []
+    for _ in range(2):
+        with rfa.SpectrumEngine(n, "blackman", "u8", ring_rows=frames) as e:
+            e.set_tuning(freq, sr)
+            e.set_channel(*chan)
+            e.process(data, frames, rows=False)
+            ring, _, _ = e.ring()
+            gpu_rows = ring[[(-g) % frames for g in range(frames)]]
+            outs.append(e.channel_means())
+    same = np.array([processor.channel_mean(r, n, freq, sr, *chan) for r in gpu_rows], np.float32)
+    np.testing.assert_allclose(outs[0], same, rtol=3e-5, atol=0)
+    np.testing.assert_array_equal(outs[0], outs[1])
 
 
 # ---------------------------------------------------------------- config 3 at its real size
