@@ -212,102 +212,6 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
     for (int b = 0; b < W::NB; b++) dft<R2>(&v[b * R2]);
 }
 
-// ---- 64 K split-staged kernel: exchange rounds that feed the next pass as they land
-// (RFA_DITX).  The four rounds of an exchange through region A used to move a
-// contiguous quarter of the positions each, so a reader had all 32 inputs only after
-// round 3, and every wave sat at the barriers while four writing waves stored a quarter:
-// the LDS exchange and the pass's arithmetic ran one after the other.
-// Here round h moves the positions p with (p >> 10) & 3 == h, i.e. a reader's inputs
-// t = 4u + h (u < 8): the pass's DFT-32 runs as decimation in time, 32 = 4 x 8 --
-// twiddle + DFT-8 over u as soon as round h has landed, while the next round's writers
-// store -- then W_32^{h k'} and a DFT-4 over h give X[k' + 8 q] (natural order).
-// Writers stay whole waves: the logical thread lt (lane_lt) puts wave bits on position
-// bits 10-11, so a round is written by four waves, one per SIMD, as before.  Part h of
-// an exchange sits in region A at 1024 (p >> 12) + (p & 1023) (+ padding).
-//   exchange 0: writer = pass-0 thread lt, outputs t0 at 32 lt + t0; reader = pass-1 thread lt
-//   exchange 1: writer = pass-1 thread lt, outputs k1 at 1024 (lt >> 5) + (lt & 31) + 32 k1;
-//               reader = pass-2 thread tid (the epilogue's store tiles keep the hardware index)
-#ifndef RFA_DITX
-#define RFA_DITX 0  // A/B only (profiles/r03/exchange_dit_rounds_ab.txt: +12 %)
-#endif
-__device__ __forceinline__ int lane_lt(int h) {
-    const int w = h >> 6, l = h & 63;
-    return (l & 31) | ((w >> 2) << 5) | ((l >> 5) << 7) | ((w & 3) << 8);
-}
-
-template <int Q, int LOGM, int PT, typename After>
-__device__ __forceinline__ void xpass_dit(float2 (&v)[PT], float2 *buf, int lt, int tid, const float2 *tw, After after) {
-    using G = WGeo<LOGM, PT>;
-    static_assert(LOGM == 15 && PT == 32 && G::TPF == 1024 && G::R1 == 32 && G::R2 == 32, "32 K items, 1024 threads");
-    int ol = lt, ot = tid;  // opaque: per-thread bases rebuilt per item, not hoisted and spilled
-    asm volatile("" : "+v"(ol), "+v"(ot));
-    const int part = __builtin_amdgcn_readfirstlane((ol >> 5) & 3);
-    constexpr int WS = Q == 0 ? 1 : 33;  // padded distance between a writer's outputs
-    const int wb = padw(1024 * (ol >> 7) + (Q == 0 ? 32 * (ol & 31) : (ol & 31)));
-    const int rd = Q == 0 ? ol : ot;  // this thread as a reader
-    const int rb = padw(rd);
-    const float2 *row1 = tw + (rd & 31) * G::P1_ROW - 1;                      // Q = 0: pass-1 table row k
-    const float2 *ra = tw + (rd / G::LO) * G::P2_ROW - 1;                    // Q = 1: A[i / 32]
-    const float2 *rbt = tw + G::TW_P2A + (rd % G::LO) * G::P2_ROW - 1;        //        B[i % 32]
-    auto write = [&] {
-#pragma unroll
-        for (int t = 0; t < 32; t++) buf[wb + WS * t] = v[t];
-    };
-    // y[h]: round h's inputs, turned in place into Y_h = DFT-8 of the twiddled inputs.
-    // A wave that has not stored its own outputs yet (part > h + 1) keeps round h raw and
-    // transforms it right after its store: it never holds its 32 outputs, the rounds
-    // read so far AND the transform's temporaries at once (no spills at 128 VGPRs).
-    float2 y[4][8];
-    auto stage1 = [&]<int h>() {
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int t = 4 * u + h;
-            if (t == 0) continue;
-            if constexpr (Q == 0) {
-                y[h][u] = cmul(y[h][u], tw_ld(row1 + t));  // W_1024^{t k}
-            } else {
-                y[h][u] = cmul(y[h][u], cmul(tw_ld(ra + t), tw_ld(rbt + t)));  // W_M^{t i} = A[i/32][t] B[i%32][t]
-            }
-        }
-        dft<8>(y[h]);
-    };
-    if (part == 0) write();
-    lds_barrier();
-    [&]<int... Hs>(std::integer_sequence<int, Hs...>) {
-        (
-            [&] {
-                constexpr int h = Hs;
-#pragma unroll
-                for (int u = 0; u < 8; u++) y[h][u] = buf[rb + 1056 * u];
-                lds_barrier();  // round h read: the region is free for round h + 1
-                if constexpr (h == 3) {
-                    after();
-                } else {
-                    if (part == h + 1) {
-                        write();
-                        // the rounds this wave deferred (all before h: part > h' + 1)
-                        [&]<int... Ds>(std::integer_sequence<int, Ds...>) {
-                            (stage1.template operator()<Ds>(), ...);
-                        }(std::make_integer_sequence<int, h>{});
-                    }
-                }
-                if (part <= h + 1) stage1.template operator()<h>();
-                if constexpr (h < 3) lds_barrier();  // round h + 1 written
-            }(),
-            ...);
-    }(std::make_integer_sequence<int, 4>{});
-    [&]<int... Ks>(std::integer_sequence<int, Ks...>) {
-        (
-            [&] {
-                constexpr int k = Ks;  // X[k + 8 q] = DFT-4 over h of Y_h[k] W_32^{h k}
-                float2 z0 = y[0][k], z1 = w64<2 * k>(y[1][k]), z2 = w64<4 * k>(y[2][k]), z3 = w64<6 * k>(y[3][k]);
-                dft4(z0, z1, z2, z3);
-                v[k] = z0, v[k + 8] = z1, v[k + 16] = z2, v[k + 24] = z3;
-            }(),
-            ...);
-    }(std::make_integer_sequence<int, 8>{});
-}
-
 // x * W_16^q added to acc, with the rotation / sqrt(1/2) forms folded in.
 template <int Q>
 __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
@@ -578,9 +482,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
-    // per-round exchange + pass (xpass_dit): the split-staged 64 K kernel, full FFT
-    constexpr bool DITX = RFA_DITX && SPLIT && (DIAG & 12) == 0;
-    const int lt = DITX ? lane_lt(threadIdx.x) : tid;  // logical thread of the pre-stage, passes 0 and 1
     static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
                            M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
     // frame of work item u (same mapping as body())
@@ -641,10 +542,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         int z;
         asm volatile("s_mov_b32 %0, 0" : "=s"(z));
         const float2 *tp1 = twp1 + z, *tp2 = twp2 + z;
-        // DITX: the logical thread, opaque per item (bases derived from it are rebuilt
-        // inside the item instead of hoisted out of the loop and spilled)
-        int lti = lt;
-        if constexpr (DITX) asm volatile("" : "+v"(lti));
         int frame, r;
         int dif_r = 0;  // large-N kernel B: column residue s of the frame (bins S q + s)
         if constexpr (RS == 1) {
@@ -711,7 +608,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
                 ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS,
                                      RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0>(
-                                v, a.window_il, a.wide_tw, in_rs, lti, planar, lraw, a.window_cw)
+                                v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
         }
@@ -729,33 +626,21 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
         }
-        // exchange 1 ends with a barrier after its last reads: the buffer is free until
-        // the next item, so the next item's frame (its second half with SPLIT) goes now
-        auto stage_next = [&] {
-            if constexpr (STG) {
-                const int fn = frame_of(unext);
-                if (unext < items && fn < a.n_frames) {
-                    if constexpr (SPLIT) stage_half(fn, 1);
-                    else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
-                }
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
+        stamp(u, 3);
+        if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
+        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
+        stamp(u, 4);
+        if constexpr (STG) {
+            // exchange 1 ended with a barrier after its last reads: the buffer is free
+            // until the next item, so stage the next item's frame now
+            const int fn = frame_of(unext);
+            if (unext < items && fn < a.n_frames) {
+                if constexpr (SPLIT) stage_half(fn, 1);
+                else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
-        };
-        if constexpr (DITX) {
-            xpass_dit<0, LOGM, PT>(v, buf, lti, tid, tp1, [] {});
-            stamp(u, 3);
-            xpass_dit<1, LOGM, PT>(v, buf, lti, tid, tp2, [&] {
-                stamp(u, 4);
-                stage_next();
-            });
-        } else {
-            if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
-            stamp(u, 3);
-            if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
-            if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
-            stamp(u, 4);
-            stage_next();
-            if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
         }
+        if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
         stamp(u, 5);
         if constexpr ((DIAG & 12) != 0) {
     #pragma unroll
