@@ -18,6 +18,7 @@
 #include <cmath>
 
 #include "fft_kernels.h"
+#include "wave.h"
 
 namespace rfa {
 
@@ -88,7 +89,7 @@ __global__ void __launch_bounds__(256) draw_rows_kernel(DrawLaunch a) {
 // (10, -100) (AppStateRepository.kt:92-93).  One workgroup; path y is NaN where
 // the reference adds no path point.
 __global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
-    __shared__ float smin[1024], smax[1024];
+    __shared__ float smin[16], smax[16];
     float mn = 10.0f, mx = -100.0f;
     for (int i = threadIdx.x; i < a.width; i += blockDim.x) {
         if (i >= a.first_pixel + 1 && i < a.last_pixel - 1) {
@@ -102,20 +103,23 @@ __global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
             a.path_y[i] = NAN;
         }
     }
-    // min / max are order independent (NaN propagates either way)
-    smin[threadIdx.x] = mn;
-    smax[threadIdx.x] = mx;
-    __syncthreads();
-    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) {
-            smin[threadIdx.x] = jmin(smin[threadIdx.x], smin[threadIdx.x + s]);
-            smax[threadIdx.x] = jmax(smax[threadIdx.x], smax[threadIdx.x + s]);
-        }
-        __syncthreads();
+    // min / max are order independent (NaN propagates either way): per wave by
+    // cross-lane moves (wave.h), then the waves' results
+    mn = wave_reduce(mn, [](float x, float y) { return jmin(x, y); });
+    mx = wave_reduce(mx, [](float x, float y) { return jmax(x, y); });
+    const int nw = (blockDim.x + 63) / 64;
+    if ((threadIdx.x & 63) == 0) {
+        smin[threadIdx.x >> 6] = mn;
+        smax[threadIdx.x >> 6] = mx;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        a.autoscale[0] = smin[0];
-        a.autoscale[1] = smax[0];
+        for (int k = 1; k < nw; k++) {
+            mn = jmin(mn, smin[k]);
+            mx = jmax(mx, smax[k]);
+        }
+        a.autoscale[0] = mn;
+        a.autoscale[1] = mx;
     }
 }
 
@@ -125,8 +129,9 @@ __global__ void __launch_bounds__(1024) draw_finish_kernel(DrawLaunch a) {
 // window [lo, hi] (inclusive bins of the fft-shifted row) the peak
 // (FloatArray.maxOrNull: NaN wins) and FloatArray.average() -- a double sum
 // divided by the count, then toFloat().  One workgroup per window; the double
-// partial sums meet in LDS (a different summation order than the JVM's
-// sequential one, equal after the final rounding to float up to one ulp).
+// partial sums meet by wavefront shuffles and then across the four waves (a different
+// summation order than the JVM's sequential one, equal after the final rounding to
+// float up to one ulp).
 __global__ void __launch_bounds__(256) row_window_kernel(const float *row, int logrs, int n, const int *lo,
                                                          const int *hi, int count, float *peak, float *avg) {
     const int w = blockIdx.x;
@@ -142,24 +147,24 @@ __global__ void __launch_bounds__(256) row_window_kernel(const float *row, int l
         mx = x > mx ? x : mx;
         s += (double)x;
     }
-    __shared__ double ss[256];
-    __shared__ float sm[256];
-    __shared__ int sn[256];
-    ss[threadIdx.x] = s;
-    sm[threadIdx.x] = mx;
-    sn[threadIdx.x] = nan;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) {
-            ss[threadIdx.x] += ss[threadIdx.x + k];
-            sm[threadIdx.x] = fmaxf(sm[threadIdx.x], sm[threadIdx.x + k]);
-            sn[threadIdx.x] |= sn[threadIdx.x + k];
-        }
-        __syncthreads();
+    // per wave by cross-lane moves (wave.h), then the four waves in order
+    s = wave_reduce(s, [](double x, double y) { return x + y; });
+    mx = wave_reduce(mx, [](float x, float y) { return fmaxf(x, y); });
+    const int anynan = wave_reduce((int)nan, [](int x, int y) { return x | y; });
+    __shared__ double ss[4];
+    __shared__ float sm[4];
+    __shared__ int sn[4];
+    if ((threadIdx.x & 63) == 0) {
+        ss[threadIdx.x >> 6] = s;
+        sm[threadIdx.x >> 6] = mx;
+        sn[threadIdx.x >> 6] = anynan;
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        peak[w] = sn[0] ? NAN : sm[0];
-        avg[w] = (float)(ss[0] / (double)(b - a + 1));
+        const double sum = ((ss[0] + ss[1]) + ss[2]) + ss[3];
+        const float m = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+        peak[w] = (sn[0] | sn[1] | sn[2] | sn[3]) ? NAN : m;
+        avg[w] = (float)(sum / (double)(b - a + 1));
     }
 }
 

@@ -23,6 +23,7 @@
 
 #include "fft_common.h"
 #include "fft_kernels.h"
+#include "wave.h"
 
 namespace rfa {
 // ----------------------------------------------------------------- geometry
@@ -635,8 +636,8 @@ hipError_t launch_state(const StateLaunch &a) {
 // FftProcessor.kt:143-157: mean of the channel's dB bins per frame (the squelch input).
 // One workgroup per frame: thread t adds bins first + t, first + t + 256, ... in that
 // order (each wave instruction reads 64 consecutive natural bins of the row), then the
-// 256 partial sums are folded in a fixed tree.  Deterministic, and within a few fp32
-// ulps of the reference's sequential fp32 loop (:150-152) -- which is itself only one
+// 256 partial sums are folded in a fixed order (wavefront shuffles, wave.h, then the
+// four waves).  Deterministic, and within a few fp32 ulps of the reference's sequential fp32 loop (:150-152) -- which is itself only one
 // rounding order of the sum; the rows it averages already differ from pffft's by up to
 // the FFT tolerance.  Round 2 kept that loop's order exactly, one lane per frame: a
 // dependent add per bin behind a load that gathers 64 rows per wave instruction,
@@ -644,7 +645,7 @@ hipError_t launch_state(const StateLaunch &a) {
 // (profiles/r03/channel_mean_ab.txt).
 __global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int first, int last, int span, float *out,
                                                           float *partial) {
-    __shared__ float part[256];
+    __shared__ float part[4];
     const int f = blockIdx.x, t = threadIdx.x;
     const float *row = state_row(a, f);
     const int lr = state_logrs(a), lm = ring_logm(lr, ilog2_dev(a.n));
@@ -658,16 +659,14 @@ __global__ void __launch_bounds__(256) channel_mean_kernel(StateLaunch a, int fi
         s = (((s + x0) + x1) + x2) + x3;
     }
     for (; i < hi; i += 256) s += row[ring_pos(i, lr, lm)];
-    part[t] = s;
+    // wave sums by cross-lane moves (wave.h), then the four waves' in order
+    s = wave_reduce(s, [](float x, float y) { return x + y; });
+    if ((t & 63) == 0) part[t >> 6] = s;
     __syncthreads();
-#pragma unroll
-    for (int h = 128; h > 0; h >>= 1) {
-        if (t < h) part[t] = part[t] + part[t + h];
-        __syncthreads();
-    }
     if (t == 0) {
-        if (gridDim.y == 1) out[f] = part[0] / (float)(last - first);
-        else partial[(size_t)f * gridDim.y + blockIdx.y] = part[0];
+        const float sum = ((part[0] + part[1]) + part[2]) + part[3];
+        if (gridDim.y == 1) out[f] = sum / (float)(last - first);
+        else partial[(size_t)f * gridDim.y + blockIdx.y] = sum;
     }
 }
 
