@@ -199,7 +199,9 @@ RFA_API int rfa_set_fft_size(rfa_handle *h, int32_t fft_size);
  * frame of each rfa_process batch, the mean dB over bins
  * [((start - f0) * (N / sampleRate.toFloat())).toInt(), same for end), each
  * clamped to [0, N], f0 = frequency - sampleRate / 2 (the tuning of
- * rfa_set_tuning).  start_frequency == end_frequency disables it.
+ * rfa_set_tuning).  start_frequency == end_frequency disables it.  The sum is a
+ * deterministic parallel reduction: equal to the reference's sequential fp32 loop
+ * (:150-152) over the same row to the rounding of the sum.
  * rfa_get_channel_means copies the last batch's means in frame order
  * (synchronises); *count = 0 when the channel range is empty. */
 RFA_API int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency);
