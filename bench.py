@@ -25,7 +25,8 @@ Multi-GPU (no data-path collective):
 
 Companions on the same line (never ``value``), run by every rank in multi-GPU
 runs with per-rank times: ``f32`` (the headline on float32 IQ), ``config2``
-(16 K cf32 Hann), ``config4`` (the shard workload), ``config5`` (a 1 M-point
+(16 K cf32 Hann), ``config4`` / ``config4_f32`` (the shard workload on s8 and cf32
+input), ``config5`` (a 1 M-point
 stream per rank), ``demod`` and, on rank 0 of a 1-GPU run, ``cpu_baseline``.
 
 Launch: ``python bench.py --gpus N`` spawns N ranks itself (one process per
@@ -732,6 +733,8 @@ def companions(args, ranks, result):
                              "unit": "Msamples/s", "ms_per_step": round(el * 1e3 / args.c2_steps, 4),
                              "kernel_ms": round(k, 4), "kernel": name, "per_rank_s": [round(x, 6) for x in per],
                              **_roof(a.frames * a.fft_size * (BPS["f32"] + 4), k)}
+        # real-time headroom = Msamples/s per stream / the source rate
+        result["config2"]["realtime_headroom"] = round(result["config2"]["value"] / W / 20.0, 1)
     if args.c4_steps > 0:
         import copy
         a4 = copy.copy(args)
@@ -751,6 +754,20 @@ def companions(args, ranks, result):
                              "us_per_batch": round(el / nb * 1e6, 3), "kernel_ms": round(k4, 4), "kernel": name4,
                              "per_rank_s": [round(x, 6) for x in per],
                              **_roof(a4.batches_per_call * mine * a4.fft_size * (BPS[a4.format] + 4), k4)}
+        # SURVEY §8(d) config 4 names f32 and s8: the same batches on complex-float32 input
+        a4.format = "f32"
+        if args.dry_run:
+            el, per = timed(ranks, lambda k: time.sleep(0.0005 * (1 + ranks.rank)), args.c4_steps, 1)
+            k4, name4 = 0.0, "dry-run"
+        else:
+            el, per, k4, name4, span, _ = run_shard(a4, ranks, args.c4_steps, 1)
+            mine = span[1] - span[0]
+        result["config4_f32"] = {"workload": f"config4 on cf32 IQ: batches of 256 x 8192-pt frames sharded over {W} "
+                                             f"GPU(s), {a4.batches_per_call} batches per rfa_process_batches call",
+                                 "value": round(total / el / 1e6, 2), "unit": "Msamples/s", "scaling": "strong",
+                                 "us_per_batch": round(el / nb * 1e6, 3), "kernel_ms": round(k4, 4), "kernel": name4,
+                                 "per_rank_s": [round(x, 6) for x in per],
+                                 **_roof(a4.batches_per_call * mine * a4.fft_size * (BPS["f32"] + 4), k4)}
     if n != (1 << 20) and args.c5_steps > 0:
         # config 5: one independent 1 M-point stream per GPU, same stateful settings
         a, el, per, k, name = _stream_companion(args, ranks, args.c5_steps, 203 + ranks.rank, fft_size=1 << 20,
@@ -763,6 +780,7 @@ def companions(args, ranks, result):
                              "kernel_ms": round(k, 4), "kernel": name, "per_rank_s": [round(x, 6) for x in per],
                              **_roof(a.frames * a.fft_size * (BPS[fmt] + 4), k),
                              "note": "kernel_ms = the whole large-N launch (front kernel + 32 K kernel B)"}
+        result["config5"]["realtime_headroom"] = round(result["config5"]["value"] / W / 250.0, 1)  # 250 Msps streams
     if ranks.rank == 0 and args.demod_steps > 0 and not args.dry_run:
         result["demod"] = demod_companion(ranks.torch, ranks.device, args.demod_steps)
 
