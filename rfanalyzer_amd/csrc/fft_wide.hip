@@ -408,32 +408,6 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #ifndef STG_POLICY
 #define STG_POLICY ""
 #endif
-// RFA_PRETOUCH (A/B builds): pull the late half of the next frame into the XCD's L2
-// early by LDS-DMA into a 1 KiB dummy slot past the kernel's LDS (every piece lands on
-// the same slot; nothing reads it), so the real DMA after exchange 1 hits L2.
-// 1: right after the pre-stage (with half 0), 2: after exchange 0.
-#ifndef RFA_PRETOUCH
-#define RFA_PRETOUCH 0
-#endif
-template <int BYTES, int THREADS>
-__device__ __forceinline__ void touch_frame(const void *src, unsigned dummy_lds) {
-    constexpr int NW = THREADS / 64, PER = BYTES / 1024 / NW;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const rsrc_t rs = make_rsrc(src, BYTES);
-#pragma unroll
-    for (int j = 0; j < PER; j++) {
-        const int c = j * NW + w;
-        unsigned keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "s"(dummy_lds), "v"(lane * 16), "s"(rs), "s"(c * 1024)
-            : "memory");
-    }
-}
-
 template <int BYTES, int THREADS>
 __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     static_assert(BYTES % (1024 * (THREADS / 64)) == 0, "whole 1 KiB pieces per wave");
@@ -521,10 +495,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int u0 = blockIdx.x;  // first item of this workgroup
     auto next_item = [&](int u) { return u + (int)gridDim.x; };
     // SPLIT: half 0 of a frame goes to region B, half 1 to region A
-    // RFA_PRETOUCH: LDS address of the 1 KiB dummy slot past the kernel's tables and buffer
-    const unsigned touch_slot =
-        (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)((uint8_t *)lds + G::LDS_BYTES);
-    (void)touch_slot;
     auto stage_half = [&](int f, int half) {
         if constexpr (SPLIT)
             stage_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0),
@@ -653,20 +623,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             stamp(u, 7);
             if constexpr (SPLIT) {  // region B is free until the next item: its half of the next frame now
                 const int fn = frame_of(unext);
-                if (unext < items && fn < a.n_frames) {
-                    stage_half(fn, 0);
-                    if constexpr (RFA_PRETOUCH == 1)
-                        touch_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride + HALF_BYTES,
-                                                            touch_slot);
-                }
+                if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
         }
         if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
-        if constexpr (SPLIT && RFA_PRETOUCH == 2) {
-            const int fn = frame_of(unext);
-            if (unext < items && fn < a.n_frames)
-                touch_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride + HALF_BYTES, touch_slot);
-        }
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
         if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
@@ -826,7 +786,7 @@ template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = f
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    const size_t lds = (size_t)G::LDS_BYTES + (RFA_PRETOUCH && STG ? 1024 : 0);
+    const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     if (RFA_CWIN && RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;
