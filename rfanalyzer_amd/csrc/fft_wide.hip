@@ -105,6 +105,12 @@ __device__ __forceinline__ float2 tw_ld(const T *p) {
     else return *p;
 }
 
+#ifndef RFA_XBASE
+#define RFA_XBASE 0  // A/B builds: per-round LDS write base in exchange Q (bit Q): 16 K s8 -3.7 %, 8 K f32 +2.6 %, 64 K +0.2 % vs the base pre-stage build (profiles/r03/xbase_ab.txt)
+#endif
+#ifndef RFA_XBASE_PRE
+#define RFA_XBASE_PRE 1  // own LDS base for the staged second half in the pre-stage: no v_add_u32 per ds_read_u16 (64 K s8 -1.5 %, profiles/r03/xbase_ab.txt; A/B builds: 0)
+#endif
 template <int Q, int LOGM, int PT, int KR = 2>
 __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
     // KR rounds (2: the M/2 buffer; 4: an M/4 buffer, RFA_SPLIT_STAGE) -- round h
@@ -120,12 +126,25 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
     const int rbase = padw(tid);                     // butterfly b adds TPF*b
     const int my_part = tid / (G::TPF / KR);         // NB == 1 writers only
+    // NB == 1: the thread's write base inside its round's part (runtime my_part, so the
+    // compiler keeps one base and immediate offsets; folding - h*PARTP into every
+    // address cost one v_add_u32 per ds_write)
+    int wloc = wbase - my_part * PARTP;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (W::NB == 1 && ((RFA_XBASE >> Q) & 1))
+        asm volatile("" : "+v"(wloc));  // built here, per item: not hoisted out of the item loop
+#endif
 #pragma unroll
     for (int h = 0; h < KR; h++) {
         if constexpr (W::NB == 1) {
             if (my_part == h) {
+                if constexpr ((RFA_XBASE >> Q) & 1) {
 #pragma unroll
-                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
+                    for (int t = 0; t < W::R; t++) buf[wloc + padw(t * W::P)] = v[t];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
+                }
             }
         } else {
 #pragma unroll
@@ -266,6 +285,12 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
         if constexpr (STG) return lds_opaque(lraw + tid);
         else return lraw;
     }();
+    // the second sample of a point (x[m + M], region A under SPLIT: a negative element
+    // offset) from its own base, so every ds_read_u16 takes an immediate offset
+    auto lraw_t1 = [&] {
+        if constexpr (STG && RS == 2 && RFA_XBASE_PRE) return lds_opaque(lraw + tid + (JS != 0 ? JS : M));
+        else return lraw_t;
+    }();
     const rsrc_t w_rs = CW ? make_rsrc(cw, M * 16) : make_rsrc(window_il, M * RS * 4);
     const rsrc_t pa_rs = make_rsrc(wide_tw + G::TW_LDS, RS * (M / 32) * 8);
     const float2 *pre_b = wide_tw + G::TW_LDS + RS * (M / 32) + R * 32;
@@ -289,7 +314,8 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG) {  // frame staged in LDS
-                    raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
+                    if (STG && RS == 2 && RFA_XBASE_PRE && j == 1) raw[s][q][j] = lraw_t1[mo];
+                    else raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
