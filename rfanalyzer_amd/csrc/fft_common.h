@@ -127,6 +127,34 @@ RFA_HD float2 cmac2(float2 a0_, float2 w0_, float2 a1_, float2 w1_) {
 #endif
 }
 
+// two independent cmac2 in one block, their chains interleaved (as cmul2): every
+// instruction's source was written two instructions earlier, so hipcc has no
+// dependent inline-asm pair to pad with s_nop (it padded each link of the single
+// cmac2 chain: 3 per point, 96 per residue-1 item)
+RFA_HD void cmac2x2(float2 &out0, float2 a0_, float2 w0_, float2 a1_, float2 w1_, float2 &out1, float2 b0_, float2 v0_,
+                    float2 b1_, float2 v1_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const f2v a0 = to_v(a0_), w0 = to_v(w0_), a1 = to_v(a1_), w1 = to_v(w1_);
+    const f2v b0 = to_v(b0_), v0 = to_v(v0_), b1 = to_v(b1_), v1 = to_v(v1_);
+    f2v m, n, r, s;
+    asm("v_pk_mul_f32 %0, %4, %5 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %1, %8, %9 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %2, %4, %5, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %3, %8, %9, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %0, %6, %7, %2 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %1, %10, %11, %3 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %2, %6, %7, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %3, %10, %11, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=&v"(m), "=&v"(n), "=&v"(r), "=&v"(s)
+        : "v"(a0), "v"(w0), "v"(a1), "v"(w1), "v"(b0), "v"(v0), "v"(b1), "v"(v1));
+    out0 = from_v(r);
+    out1 = from_v(s);
+#else
+    out0 = cmac2(a0_, w0_, a1_, w1_);
+    out1 = cmac2(b0_, v0_, b1_, v1_);
+#endif
+}
+
 // complex a * (c, s) for a compile-time constant (held in an SGPR pair)
 // (plain vector code: both constant pairs live in SGPRs, hipcc emits v_pk_mul +
 // v_pk_fma and is free to interleave independent multiplies)

@@ -259,6 +259,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_CWIN
 #define RFA_CWIN 1  // N = 64 K residue 1: twiddle folded into a complex window (A/B builds: 0 = separate)
 #endif
+#ifndef RFA_CMAC2X2
+#define RFA_CMAC2X2 1  // residue-1 complex-window pre-stage as interleaved point pairs (A/B builds: 0 = one chain per point)
+#endif
 #ifndef RFA_TILE
 #define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
 #endif
@@ -350,10 +353,19 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     auto compute = [&]<int c>() {
         constexpr int s = c % (DIST + 1);
         if constexpr (CW) {  // y_1[m] = x[m] cw0[m] + x[m + M] cw1[m]   (NativeDsp.kt:55-58 window, DIF twiddle)
+            if constexpr (RFA_CMAC2X2 && STG && C % 2 == 0) {  // two points' chains interleaved (fft_common.h cmac2x2)
 #pragma unroll
-            for (int q = 0; q < C; q++)
-                v[c * C + q] = cmac2(convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
-                                     convert_raw<FMT>(raw[s][q][1]), make_float2(win[s][q][2], win[s][q][3]));
+                for (int q = 0; q < C; q += 2)
+                    cmac2x2(v[c * C + q], convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
+                            convert_raw<FMT>(raw[s][q][1]), make_float2(win[s][q][2], win[s][q][3]), v[c * C + q + 1],
+                            convert_raw<FMT>(raw[s][q + 1][0]), make_float2(win[s][q + 1][0], win[s][q + 1][1]),
+                            convert_raw<FMT>(raw[s][q + 1][1]), make_float2(win[s][q + 1][2], win[s][q + 1][3]));
+            } else {
+#pragma unroll
+                for (int q = 0; q < C; q++)
+                    v[c * C + q] = cmac2(convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
+                                         convert_raw<FMT>(raw[s][q][1]), make_float2(win[s][q][2], win[s][q][3]));
+            }
             return;
         } else if constexpr (RS == 2 && R == 0 && !NOWIN) {  // y_0[m] = x[m] w[m] + x[m + M] w[m + M] (mul + fma)
 #pragma unroll
