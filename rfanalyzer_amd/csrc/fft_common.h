@@ -155,6 +155,37 @@ RFA_HD void cmac2x2(float2 &out0, float2 a0_, float2 w0_, float2 a1_, float2 w1_
 #endif
 }
 
+// Large-N front-kernel twiddle for two outputs: v_k *= C_k + C_k * D_k, with the
+// wave-uniform C_k in SGPR pairs (scalar loads) and D_k per lane; the two chains are
+// interleaved so no packed result is read by the next instruction (as cmul2), and a
+// VOP3P instruction reads one SGPR pair at most (constant-bus limit).
+RFA_HD void twiddle_cd2(float2 &v0_, float2 d0_, float2 c0_, float2 &v1_, float2 d1_, float2 c1_) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    f2v v0 = to_v(v0_), v1 = to_v(v1_);
+    const f2v d0 = to_v(d0_), d1 = to_v(d1_), c0 = to_v(c0_), c1 = to_v(c1_);
+    f2v m0, m1, r0, r1;
+    asm("v_pk_mul_f32 %0, %8, %6 op_sel_hi:[0,1]\n\t"  // C * D as cmul(C, D): same products and rounding
+        "v_pk_mul_f32 %1, %9, %7 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %2, %8, %6, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %3, %9, %7, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_add_f32 %2, %2, %8\n\t"
+        "v_pk_add_f32 %3, %3, %9\n\t"
+        "v_pk_mul_f32 %0, %4, %2 op_sel_hi:[0,1]\n\t"
+        "v_pk_mul_f32 %1, %5, %3 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %4, %4, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+        "v_pk_fma_f32 %5, %5, %3, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=&v"(m0), "=&v"(m1), "=&v"(r0), "=&v"(r1), "+v"(v0), "+v"(v1)
+        : "v"(d0), "v"(d1), "s"(c0), "s"(c1));
+    v0_ = from_v(v0);
+    v1_ = from_v(v1);
+#else
+    const float2 k0 = cmul(c0_, d0_), k1 = cmul(c1_, d1_);
+    const float2 w0 = make_float2(c0_.x + k0.x, c0_.y + k0.y), w1 = make_float2(c1_.x + k1.x, c1_.y + k1.y);
+    v0_ = cmul(v0_, w0);
+    v1_ = cmul(v1_, w1);
+#endif
+}
+
 // complex a * (c, s) for a compile-time constant (held in an SGPR pair)
 // (plain vector code: both constant pairs live in SGPRs, hipcc emits v_pk_mul +
 // v_pk_fma and is free to interleave independent multiplies)

@@ -32,6 +32,9 @@
 
 namespace rfa {
 
+#ifndef RFA_DIF_SMEM
+#define RFA_DIF_SMEM 1  // pipelined front kernel: C twiddle factors by scalar loads (A/B builds: 0)
+#endif
 #ifndef RFA_DIF_ABL
 #define RFA_DIF_ABL 0  // ablations (A/B builds only): 1 no z stores, 2 no twiddles
 #endif
@@ -165,6 +168,10 @@ __global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int gr
 #pragma unroll
     for (int j = 0; j < S; j++) w[j] = buf_load_f32(w_rs, m * 4, j * M * 4);
     const int khi = __builtin_amdgcn_readfirstlane(m >> 7), klo = m & 127;
+    // C factors through the constant address space: the index is wave-uniform, so they
+    // are scalar loads (s_load_dwordx2) instead of a uniform-address VMEM load per s
+    const auto *tw_c_s = (const __attribute__((address_space(4))) f2v *)(uintptr_t)a.tw_c;
+    auto c_at = [&](int i) { return from_v(tw_c_s[i]); };
     if (g0 < a.n_frames) stage(g0);
     bool first = true;
     for (int f = g0; f < a.n_frames; f += groups) {
@@ -182,10 +189,21 @@ __global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int gr
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave has read the tile
         if (f + groups < a.n_frames) stage(f + groups);
         dft<S>(v);
+        if constexpr (RFA_DIF_SMEM) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel; C in SGPRs
+            {
+                const float2 c = c_at(mc + khi), corr = cmul(c, dtab[128 + klo]);
+                v[1] = cmul(v[1], make_float2(c.x + corr.x, c.y + corr.y));
+            }
 #pragma unroll
-        for (int s = 1; s < S; s++) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel
-            const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, dtab[s * 128 + klo]);
-            v[s] = cmul(v[s], make_float2(c.x + corr.x, c.y + corr.y));
+            for (int s = 2; s < S; s += 2)
+                twiddle_cd2(v[s], dtab[s * 128 + klo], c_at(s * mc + khi), v[s + 1], dtab[(s + 1) * 128 + klo],
+                            c_at((s + 1) * mc + khi));
+        } else {
+#pragma unroll
+            for (int s = 1; s < S; s++) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel
+                const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, dtab[s * 128 + klo]);
+                v[s] = cmul(v[s], make_float2(c.x + corr.x, c.y + corr.y));
+            }
         }
         const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
 #pragma unroll
