@@ -490,6 +490,21 @@ __device__ __forceinline__ float2 buf_load_f32x2(rsrc_t rs, int voff, int soff) 
 __device__ __forceinline__ void buf_store_f32(float x, rsrc_t rs, int voff, int soff) {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, x), rs, voff, soff, 0);
 }
+// dword store at a compile-time byte offset SO: the SGPR offset is set by an s_mov_b32
+// next to the store (SALU: no VALU-write-SGPR hazard before the VMEM read), so hipcc
+// cannot hoist a kernel's worth of distinct offsets out of a loop and spill them
+template <int SO>
+__device__ __forceinline__ void buf_store_f32_c(float x, rsrc_t rs, int voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int so;
+    asm volatile("s_mov_b32 %0, %3\n\tbuffer_store_dword %1, %2, %4, %0 offen"
+                 : "=&s"(so)
+                 : "v"(x), "v"(voff), "i"(SO), "s"(rs)
+                 : "memory");
+#else
+    (void)x; (void)rs; (void)voff;
+#endif
+}
 #ifndef RFA_X4_POLICY
 #define RFA_X4_POLICY ""  // cache policy of the 16-B ring stores (A/B builds: "nt", "sc1")
 #endif

@@ -262,6 +262,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_CMAC2X2
 #define RFA_CMAC2X2 1  // residue-1 complex-window pre-stage as interleaved point pairs (A/B builds: 0 = one chain per point)
 #endif
+#ifndef RFA_DIF_CSO
+#define RFA_DIF_CSO 1  // large-N kernel B epilogue with compile-time store offsets (A/B builds: 0)
+#endif
 #ifndef RFA_TILE
 #define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
 #endif
@@ -765,6 +768,23 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 }
             }
             auto epilogue = [&](auto nat_c, auto ring_c, auto rm_c) {
+                if constexpr (dif && RFA_DIF_CSO && (DIAG & 2) == 0) {
+                    // large-N kernel B: every store offset is a compile-time constant (residue-major
+                    // rows and ring); one s_mov_b32 next to each store instead of 32 offsets hoisted
+                    // out of the item loop, spilled to VGPR lanes and read back with v_readlane + s_nop 4
+                    [&]<int... Is>(std::integer_sequence<int, Is...>) {
+                        (
+                            [&] {
+                                constexpr int b = Is / G::R2, t = Is % G::R2;
+                                constexpr int so_rm = ((G::TPF * b + t * (M / G::R2) + M / 2) & (M - 1)) * 4;
+                                const float db = db_unscaled(v[Is], db_off);  // nativedsp.cpp:73-78
+                                if constexpr (decltype(nat_c)::value) buf_store_f32_c<so_rm>(db, row_rs, tid * 4);
+                                if constexpr (decltype(ring_c)::value) buf_store_f32_c<so_rm>(db, ring_rs, tid * 4);
+                            }(),
+                            ...);
+                    }(std::make_integer_sequence<int, PT>{});
+                    return;
+                }
     #pragma unroll
                 for (int b = 0; b < PT / G::R2; b++) {
     #pragma unroll
