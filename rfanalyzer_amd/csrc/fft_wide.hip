@@ -265,6 +265,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_DIF_CSO
 #define RFA_DIF_CSO 1  // large-N kernel B epilogue with compile-time store offsets (A/B builds: 0)
 #endif
+#ifndef RFA_QSTAGE
+#define RFA_QSTAGE 1  // 64 K interleaved cf32: stage the next frame's first quarter of each half (QST)
+#endif
 #ifndef RFA_TILE
 #define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
 #endif
@@ -275,7 +278,8 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // costs two complex multiply-adds (cmac2: 4 packed instructions) instead of two window
 // products, a subtraction and two complex multiplies (7).  (f32 input keeps the separate
 // twiddle: its 8-B raw samples and the 16-B window pairs in flight would spill.)
-template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int JS = 0, bool CW = false>
+template <int LOGM, int PT, int RS, int FMT, int R, bool STG = false, bool NOWIN = false, int JS = 0, bool CW = false,
+          int QCH = 0>
 __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il, const float2 *wide_tw, rsrc_t in_rs,
                                          int tid, int planar_im, const typename Raw<FMT>::T *lraw = nullptr,
                                          const float4 *cw = nullptr) {
@@ -319,7 +323,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
 #pragma unroll
             for (int j = 0; j < RS; j++) {
-                if constexpr (STG) {  // frame staged in LDS
+                if constexpr (STG && (QCH == 0 || c < QCH)) {  // frame (QCH: its first QCH chunks) staged in LDS
                     if (STG && RS == 2 && RFA_XBASE_PRE && j == 1) raw[s][q][j] = lraw_t1[mo];
                     else raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
                 }
@@ -518,13 +522,28 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // region B right after this item's pre-stage (it flies during both exchanges and
     // passes) and only its second half waits for exchange 1 (into A).
     constexpr bool SPLIT = STG && RS == 2 && LOGM == 15 && BPS == 2 && !COMPLEX_OUT;
+    // QST (64 K interleaved cf32): only the first QN points of each half of the next frame
+    // (x[0, QN) and x[M, M + QN), 64 KB each) are staged after exchange 1; the pre-stage
+    // reads its first QCH chunks from LDS and the rest from memory as before
+    constexpr bool QST = STG && FMT == 3 && RS == 2 && LOGM == 15 && !COMPLEX_OUT;
+    constexpr int QN = M / 4, QCH = QST ? QN / (M / 32) / ((PT == 64 ? 16 : 8) / RS) : 0;
+    constexpr int Q_BYTES = QN * 8;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
     constexpr int KR = SPLIT ? 4 : 2;                // exchange rounds
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
-    static_assert(!STG || (G::SLOTS == 1 && FMT <= 2 && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
-                           M * RS * BPS <= G::HALFP * 8), "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer");
+    static_assert(!STG || (G::SLOTS == 1 && (FMT <= 2 || QST) && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
+                           (QST ? 2 * QN <= G::HALFP : M * RS * BPS <= G::HALFP * 8)),
+                  "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer (or QST's two cf32 quarters)");
+    static_assert(!QST || QCH * ((PT == 64 ? 16 : 8) / RS) * (M / 32) == QN, "QST: whole pre-stage chunks");
+    auto stage_q = [&](int f) {  // QST: the two staged pieces of frame f
+        if constexpr (QST) {
+            const uint8_t *fb = a.in + (size_t)f * (size_t)a.frame_stride;
+            stage_frame<Q_BYTES, G::THREADS>(fb, buf);
+            stage_frame<Q_BYTES, G::THREADS>(fb + (size_t)M * 8, buf + QN);
+        }
+    };
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
         if constexpr (RS == 1) return u;
@@ -547,6 +566,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if constexpr (SPLIT) {
                 stage_half(f0, 0);
                 stage_half(f0, 1);
+            } else if constexpr (QST) {
+                stage_q(f0);
             } else {
                 stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
             }
@@ -647,8 +668,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
-                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, JS,
-                                     RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0>(
+                ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, QST ? QN : JS,
+                                     RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0, QCH>(
                                 v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
@@ -678,6 +699,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             const int fn = frame_of(unext);
             if (unext < items && fn < a.n_frames) {
                 if constexpr (SPLIT) stage_half(fn, 1);
+                else if constexpr (QST) stage_q(fn);
                 else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
@@ -901,6 +923,9 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         }
         if constexpr (stg16) {
             if (stg && a.fmt == 2) return launch_wide_one<LOGM, PT, RS, 2, false, 0, true>(a);
+        }
+        if constexpr (RFA_QSTAGE && LOGM == 15 && RS == 2 && G::SLOTS == 1) {  // cf32 64 K: quarter staging (QST)
+            if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
         switch (a.fmt) {
         case 0: return launch_wide_one<LOGM, PT, RS, 0, false>(a);
