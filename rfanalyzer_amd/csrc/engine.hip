@@ -261,7 +261,7 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         B.complex_out = a.complex_out ? a.complex_out + (size_t)f0 * n : nullptr;
         B.ring_base = a.ring_base - f0;  // frame f0 + f of the call is frame f of this pair
         B.ring_first = a.ring_first - f0;
-        B.stage = 0;
+        B.stage = h->stage;  // kernel B stages half of its next item's z_s (fft_wide.hip QSTB)
         B.diag = 0;
         B.stamps = nullptr;
         e = rfa::launch_fft_wide(B);

@@ -268,6 +268,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_QSTAGE
 #define RFA_QSTAGE 1  // 64 K interleaved cf32: stage the next frame's first quarter of each half (QST)
 #endif
+#ifndef RFA_QSTAGE_B
+#define RFA_QSTAGE_B 1  // large-N kernel B: stage the first half of the next item's z_s (QSTB)
+#endif
 #ifndef RFA_TILE
 #define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
 #endif
@@ -528,15 +531,25 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     constexpr bool QST = STG && FMT == 3 && RS == 2 && LOGM == 15 && !COMPLEX_OUT;
     constexpr int QN = M / 4, QCH = QST ? QN / (M / 32) / ((PT == 64 ? 16 : 8) / RS) : 0;
     constexpr int Q_BYTES = QN * 8;
+    // QSTB (large-N kernel B): the first half of the next item's z_s (M/2 points, 128 KB)
+    // is staged after exchange 1; its pass-0 loads t < 16 read LDS, the rest memory
+    constexpr bool QSTB = STG && dif;
+    constexpr int QB_BYTES = (M / 2) * 8;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
     constexpr int KR = SPLIT ? 4 : 2;                // exchange rounds
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
-    static_assert(!STG || (G::SLOTS == 1 && (FMT <= 2 || QST) && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
-                           (QST ? 2 * QN <= G::HALFP : M * RS * BPS <= G::HALFP * 8)),
+    static_assert(!STG || (G::SLOTS == 1 && (FMT <= 2 || QST || QSTB) && !COMPLEX_OUT && (DIAG & STG_DIAG_OK) == 0 &&
+                           (QST ? 2 * QN <= G::HALFP : QSTB ? M / 2 <= G::HALFP : M * RS * BPS <= G::HALFP * 8)),
                   "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer (or QST's two cf32 quarters)");
     static_assert(!QST || QCH * ((PT == 64 ? 16 : 8) / RS) * (M / 32) == QN, "QST: whole pre-stage chunks");
+    auto stage_qb = [&](int u) {  // QSTB: the first half of item u's column block z_s
+        if constexpr (QSTB) {
+            const int fr = u / a.dif_ss, sr = u - fr * a.dif_ss;
+            stage_frame<QB_BYTES, G::THREADS>(a.in + (size_t)fr * (size_t)a.frame_stride + (size_t)sr * (M * 8), buf);
+        }
+    };
     auto stage_q = [&](int f) {  // QST: the two staged pieces of frame f
         if constexpr (QST) {
             const uint8_t *fb = a.in + (size_t)f * (size_t)a.frame_stride;
@@ -546,7 +559,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     };
     // frame of work item u (same mapping as body())
     auto frame_of = [&](int u) {
-        if constexpr (RS == 1) return u;
+        if constexpr (dif) return u / a.dif_ss;  // kernel B: item = (frame, column block)
+        else if constexpr (RS == 1) return u;
         else return (u / (8 * RS)) * 8 + (u & 7);
     };
     // Work distribution: items blockIdx.x, + grid, ... (static: the residues of a frame
@@ -568,6 +582,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 stage_half(f0, 1);
             } else if constexpr (QST) {
                 stage_q(f0);
+            } else if constexpr (QSTB) {
+                stage_qb(u0);
             } else {
                 stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)f0 * (size_t)a.frame_stride, buf);
             }
@@ -652,8 +668,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             for (int idx = 0; idx < PT; idx++) {
                 const int so = G::TPF * (idx >> 5) + (M / 32) * (idx & 31);
                 if constexpr (DIAG & 1) raw[idx] = synth_raw<FMT>(so + tid);
-                else if constexpr (STG) raw[idx] = lraw[so + tid];
-                else raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
+                else if constexpr (STG) {
+                    if (QSTB && idx >= PT / 2) raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
+                    else raw[idx] = lraw[so + tid];
+                } else raw[idx] = buf_load_raw<FMT>(in_rs, tid * SB, so * SB, planar_im);
             }
     #pragma unroll
             for (int idx = 0; idx < PT; idx++) {
@@ -700,6 +718,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if (unext < items && fn < a.n_frames) {
                 if constexpr (SPLIT) stage_half(fn, 1);
                 else if constexpr (QST) stage_q(fn);
+                else if constexpr (QSTB) stage_qb(unext);
                 else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
@@ -1018,7 +1037,11 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
 #endif
     if (a.fmt == kFmtDif) {  // kernel B of the large-N pair (dB rows / ring, or the ordered spectrum)
         if (a.dif_ss < 8 || a.dif_ss > 32) return hipErrorInvalidValue;
-        return co ? launch_wide_one<kDitLogM, 32, 1, kFmtDif, true>(a) : launch_wide_one<kDitLogM, 32, 1, kFmtDif, false>(a);
+        if (co) return launch_wide_one<kDitLogM, 32, 1, kFmtDif, true>(a);
+        // QSTB: half of the next item's z_s staged by LDS-DMA (16-byte aligned scratch)
+        if (RFA_QSTAGE_B && a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0)
+            return launch_wide_one<kDitLogM, 32, 1, kFmtDif, false, 0, true>(a);
+        return launch_wide_one<kDitLogM, 32, 1, kFmtDif, false>(a);
     }
     switch (a.logn) {
     case 13: return co ? wide_by_fmt<13, 32, 1, true>(a) : wide_by_fmt<13, 32, 1, false>(a);
