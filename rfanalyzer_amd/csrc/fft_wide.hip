@@ -268,6 +268,9 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #ifndef RFA_QSTAGE
 #define RFA_QSTAGE 1  // 64 K interleaved cf32: stage the next frame's first quarter of each half (QST)
 #endif
+#ifndef RFA_QSTAGE_H
+#define RFA_QSTAGE_H 0  // interleaved cf32 at 8 K .. 32 K: stage the first half of the next frame (QSTB)
+#endif
 #ifndef RFA_QSTAGE_B
 #define RFA_QSTAGE_B 1  // large-N kernel B: stage the first half of the next item's z_s (QSTB)
 #endif
@@ -531,9 +534,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     constexpr bool QST = STG && FMT == 3 && RS == 2 && LOGM == 15 && !COMPLEX_OUT;
     constexpr int QN = M / 4, QCH = QST ? QN / (M / 32) / ((PT == 64 ? 16 : 8) / RS) : 0;
     constexpr int Q_BYTES = QN * 8;
-    // QSTB (large-N kernel B): the first half of the next item's z_s (M/2 points, 128 KB)
-    // is staged after exchange 1; its pass-0 loads t < 16 read LDS, the rest memory
-    constexpr bool QSTB = STG && dif;
+    // QSTB (one-residue items on 8-byte complex input: large-N kernel B's z_s, or
+    // interleaved cf32 frames of 8 K ... 32 K points): the first half of the next item's
+    // points (M/2, 4 M bytes) is staged after exchange 1; its pass-0 loads t < 16 read
+    // LDS, the rest memory
+    constexpr bool QSTB = STG && RS == 1 && (dif || FMT == 3) && !COMPLEX_OUT;
     constexpr int QB_BYTES = (M / 2) * 8;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
     constexpr int KR = SPLIT ? 4 : 2;                // exchange rounds
@@ -544,10 +549,14 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                            (QST ? 2 * QN <= G::HALFP : QSTB ? M / 2 <= G::HALFP : M * RS * BPS <= G::HALFP * 8)),
                   "STG: one sub-FFT per WG, 8/16-bit input fitting the buffer (or QST's two cf32 quarters)");
     static_assert(!QST || QCH * ((PT == 64 ? 16 : 8) / RS) * (M / 32) == QN, "QST: whole pre-stage chunks");
-    auto stage_qb = [&](int u) {  // QSTB: the first half of item u's column block z_s
+    auto stage_qb = [&](int u) {  // QSTB: the first half of item u's points (kernel B: of its column block z_s)
         if constexpr (QSTB) {
-            const int fr = u / a.dif_ss, sr = u - fr * a.dif_ss;
-            stage_frame<QB_BYTES, G::THREADS>(a.in + (size_t)fr * (size_t)a.frame_stride + (size_t)sr * (M * 8), buf);
+            if constexpr (dif) {
+                const int fr = u / a.dif_ss, sr = u - fr * a.dif_ss;
+                stage_frame<QB_BYTES, G::THREADS>(a.in + (size_t)fr * (size_t)a.frame_stride + (size_t)sr * (M * 8), buf);
+            } else {
+                stage_frame<QB_BYTES, G::THREADS>(a.in + (size_t)u * (size_t)a.frame_stride, buf);
+            }
         }
     };
     auto stage_q = [&](int f) {  // QST: the two staged pieces of frame f
@@ -944,6 +953,9 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
             if (stg && a.fmt == 2) return launch_wide_one<LOGM, PT, RS, 2, false, 0, true>(a);
         }
         if constexpr (RFA_QSTAGE && LOGM == 15 && RS == 2 && G::SLOTS == 1) {  // cf32 64 K: quarter staging (QST)
+            if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
+        }
+        if constexpr (RFA_QSTAGE_H && RS == 1 && G::SLOTS == 1) {  // cf32 8 K .. 32 K: half staging (QSTB)
             if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
         switch (a.fmt) {
