@@ -269,7 +269,7 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 #define RFA_QSTAGE 1  // 64 K interleaved cf32: stage the next frame's first quarter of each half (QST)
 #endif
 #ifndef RFA_QSTAGE_H
-#define RFA_QSTAGE_H 0  // interleaved cf32 at 8 K .. 32 K: stage the first half of the next frame (QSTB)
+#define RFA_QSTAGE_H 0  // A/B builds: QSTB half staging for interleaved cf32 at 8 K / 16 K too (32 K always)
 #endif
 #ifndef RFA_QSTAGE_B
 #define RFA_QSTAGE_B 1  // large-N kernel B: stage the first half of the next item's z_s (QSTB)
@@ -955,7 +955,8 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         if constexpr (RFA_QSTAGE && LOGM == 15 && RS == 2 && G::SLOTS == 1) {  // cf32 64 K: quarter staging (QST)
             if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
-        if constexpr (RFA_QSTAGE_H && RS == 1 && G::SLOTS == 1) {  // cf32 8 K .. 32 K: half staging (QSTB)
+        // cf32 32 K: half staging (QSTB); at 8 K / 16 K it spills and is slower (profiles/r03/qstage_h_ab.txt)
+        if constexpr ((RFA_QSTAGE_H || LOGM == 15) && RS == 1 && G::SLOTS == 1) {
             if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
         switch (a.fmt) {
