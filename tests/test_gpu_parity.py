@@ -55,6 +55,20 @@ def test_all_sizes_and_formats_vs_oracle(rfa, n, fmt):
     gu.assert_same_peak_bins(rows, np.argmax(ref, 1))
 
 
+@pytest.mark.parametrize("n,frames", [(65536, 160), (32768, 300)])
+def test_cf32_staged_next_item_across_workgroup_items(rfa, n, frames):
+    """Interleaved cf32 at 32 K / 64 K stages part of each workgroup's NEXT item by LDS-DMA
+    (fft_wide.hip QSTB / QST; persistent grid of one workgroup per CU): with more items than
+    workgroups every workgroup runs 2-3 items, so a staged piece of the wrong frame or residue
+    would show in some row.  Every row vs the float64 oracle."""
+    data = signals.frames_bytes(n, frames, "f32", seed=frames, tones=((0.173, 0.5), (-0.29, 0.01)), noise=0.03)
+    with _engine(rfa, n, "f32", "blackman", ring_rows=0) as e:
+        rows = e.process(data, frames)
+    ref = oracle.spectrum_rows(data, signals.FORMATS["f32"], n, frames, None, oracle.WIN_BLACKMAN)
+    assert gu.db_diff(rows, ref) <= gu.DB_TOL
+    gu.assert_same_peak_bins(rows, np.argmax(ref, 1))
+
+
 def test_hann_config2_signal(rfa):
     """Config 2: 20 Msps cf32, N=16384, Hann (oracle = float64 restatement)."""
     n, b = 16384, 64
