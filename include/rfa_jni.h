@@ -48,6 +48,20 @@
 extern "C" {
 #endif
 
+/* JNI surface version.  2 (round 3): frame_stride 0 of processIqBytesNative /
+ * processPacketNative is the reference's packet framing (one frame per completing packet,
+ * the rest of that packet dropped); version 1 read 0 as "every whole frame, densely
+ * packed" -- callers of that form pass frame_stride = fft_size * bytes per sample. */
+#define RFA_JNI_ABI_VERSION 2
+JNIEXPORT int rfa_jni_abi_version(void);
+/* Status of the last legacy call (performFFT, performFFTAndLogMag,
+ * performWindowedFftAndReturnMagNative, processIqBytesNative), whose JNI signatures
+ * return nothing (nativedsp.cpp:19-81): RFA_OK, or e.g. RFA_ERR_UNSUPPORTED when the
+ * length is one the reference's pffft accepts (N = 2^a 3^b 5^c, a multiple of 16,
+ * pffft.c:1236-1247) but librfa does not (N a power of two, 64 .. 2^20) -- the output
+ * array is then left untouched. */
+JNIEXPORT int rfa_jni_last_status(void);
+
 JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFT(JNIEnv *env, jobject thiz,
                                                                           jfloatArray input, jfloatArray output);
 JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFTAndLogMag(JNIEnv *env, jobject thiz,

@@ -36,6 +36,7 @@ struct rfa_handle {
     float *d_window_il = nullptr;     // N > 32768: scaled window as [m][j], m < 32768, j < N/32768
     float4 *d_window_cw = nullptr;    // N = 65536: (w[m] W_N^m, -w[m+M] W_N^m), residue 1 of the pre-stage
     float2 *d_wide_tw = nullptr;      // wide-kernel twiddle blob (N = 2^13..2^17, and kernel A for larger N)
+    float2 *d_w64_tw = nullptr;       // N = 64 K: the wave-decoupled kernel's twiddle blob (fft_w64.hip)
     // N = 2^18..2^20 (decimation in frequency, fft_large.hip)
     float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{m s} = C[s][m >> 7] * D[s][m & 127]
     float2 *d_dit_y = nullptr;        // scratch z [frames][S][M] complex
@@ -288,6 +289,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         a.stamps = h->d_stamps;
     }
     a.wide_tw = h->d_wide_tw;
+    a.w64_tw = h->d_w64_tw;
     a.variant = h->variant;
     if (a.window == h->d_window) {
         a.window_il = h->d_window_il;
@@ -483,6 +485,12 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         const size_t mb = 128;
         h->dit_frames = (int)std::max<size_t>(1, (mb << 20) / ((size_t)n * sizeof(float2)));
     }
+    if (logn == 16) {
+        std::vector<float2> blob = rfa::w64_twiddles();
+        if (hipMalloc(&h->d_w64_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
+        if (hipMemcpy(h->d_w64_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)
+            return bail(RFA_ERR_HIP);
+    }
     if (rfa::wide_supported(logn)) {
         std::vector<float2> blob = rfa::wide_twiddles(logn, rfa::kWidePT, rfa::wide_logm(logn));
         if (hipMalloc(&h->d_wide_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
@@ -562,6 +570,7 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_window_il);
     hipFree(h->d_window_cw);
     hipFree(h->d_wide_tw);
+    hipFree(h->d_w64_tw);
     hipFree(h->d_dit_c);
     hipFree(h->d_dit_d);
     hipFree(h->d_dit_y);

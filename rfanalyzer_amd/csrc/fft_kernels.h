@@ -34,14 +34,30 @@ __host__ __device__ __forceinline__ int tile_pos(int i) {  // i' -> storage posi
 __host__ __device__ __forceinline__ int tile_sub(int p) {  // inverse of tile_pos
     return ((((p >> 8) & 7) << 2 | (p & 3)) << 10) | ((p >> 11) << 6) | ((p >> 2) & 63);
 }
+// bit 9 (kRingTile2, N = 64 K only): the store tiles of the wave-decoupled 64 K kernel
+// (fft_w64.hip).  Its sub-bin i' = k0 + 32 k1 + 1024 t' (k0, k1 < 32: the output digits the
+// kernel's exchanges leave in lane bit 0 + wave bits and in lane bits 1-5) is held by lane
+// l = (k0 & 1) | (k1 << 1) of wave w = k0 >> 1 in register t'; a thread's four registers
+// t' = 4j .. 4j+3 are one 16-B store at w*2048 + j*256 + l*4 -- the same store geometry as
+// kRingTile with a different (lane, wave) <-> bin assignment.
+constexpr int kRingTile2 = 0x200;
+__host__ __device__ __forceinline__ int tile2_pos(int i) {
+    const int k0 = i & 31, k1 = (i >> 5) & 31, tp = i >> 10;
+    return ((k0 >> 1) << 11) | ((tp >> 2) << 8) | (((k0 & 1) | (k1 << 1)) << 2) | (tp & 3);
+}
+__host__ __device__ __forceinline__ int tile2_sub(int p) {
+    const int w = p >> 11, j = (p >> 8) & 7, l = (p >> 2) & 63, e = p & 3;
+    return ((l & 1) | (w << 1)) | ((l >> 1) << 5) | ((4 * j + e) << 10);
+}
 __host__ __device__ __forceinline__ int ring_pos(int t, int code, int logm) {
     const int lr = code & 0xff, sub = t >> lr;
-    return ((t & ((1 << lr) - 1)) << logm) | ((code & kRingTile) ? tile_pos(sub) : sub);
+    return ((t & ((1 << lr) - 1)) << logm) |
+           ((code & kRingTile) ? tile_pos(sub) : (code & kRingTile2) ? tile2_pos(sub) : sub);
 }
 // inverse: the natural (fft-shifted) bin stored at ring element p
 __host__ __device__ __forceinline__ int ring_bin(int p, int code, int logm) {
     const int lr = code & 0xff, q = p & ((1 << logm) - 1);
-    return (((code & kRingTile) ? tile_sub(q) : q) << lr) | (p >> logm);
+    return (((code & kRingTile) ? tile_sub(q) : (code & kRingTile2) ? tile2_sub(q) : q) << lr) | (p >> logm);
 }
 
 // Largest sub-FFT one workgroup keeps resident in LDS (16384 complex fp32 =
@@ -65,6 +81,7 @@ struct FftLaunch {
     // wide kernel twiddle blob (exact, from double): pass-1 [32][R1] | pass-2 A,B [16][16] |
     // pre-stage pre_a [RS][512] | pre_b [RS][32]   (DESIGN.md "Twiddles")
     const float2 *wide_tw = nullptr;  // wide_twiddles() blob (layout in fft_wide.hip WGeo)
+    const float2 *w64_tw = nullptr;   // N = 64 K: w64_twiddles() blob of the wave-decoupled kernel (fft_w64.hip)
     // twiddle table W_N^s = coarse[s >> tw_shift] * fine[s & ((1<<tw_shift)-1)]
     const float2 *tw_coarse = nullptr;
     const float2 *tw_fine = nullptr;
@@ -107,6 +124,10 @@ constexpr int kWidePT = 32;  // wide kernel: points per thread (32 an
 inline int wide_logm(int logn) { return logn <= 14 ? logn : 15; }
 std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
+// N = 64 K (dB rows / ring; not the complex-out seam): the wave-decoupled kernel, one
+// cross-wave exchange per 32 K residue item (fft_w64.hip)
+std::vector<float2> w64_twiddles();
+hipError_t launch_fft64(const FftLaunch &a);
 
 // N = 2^18 .. 2^20: decimation-in-frequency pair (DESIGN.md "Large N", fft_large.hip).
 // Kernel A (dif_front_kernel) converts and windows the S = N / 32768 columns

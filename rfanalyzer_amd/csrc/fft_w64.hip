@@ -1,0 +1,451 @@
+// gfx950 64 K-point kernel, wave-decoupled form.
+//
+// Same per-frame pipeline as the wide kernel (fft_wide.hip): raw IQ -> LUT-exact convert ->
+// window (fp32 multiply, NativeDsp.kt:55-58) -> radix-2 decimation-in-frequency pre-stage
+// into two 32 K residue items -> FFT (sign -1, unscaled, pffft.h:117) -> 10*log10(|X|/N) +
+// fft-shift (nativedsp.cpp:72-79) -> ring / rows.  What differs is how the 16 waves of the
+// 1024-thread workgroup that holds one 32 K item are coupled:
+//
+//   * index bits: m = m0 + 32 m1 + 1024 m2 (5-bit digits).  At pass 0 a thread holds m2 in
+//     its 32 registers; lane bits 1-5 carry m0 and lane bit 0 + the 4 wave bits carry m1.
+//     Pass 0 (DFT over m2 -> k0), exchange 0, pass 1 (m1 -> k1), exchange 1, pass 2
+//     (m0 -> k2): X[k0 + 32 k1 + 1024 k2] (DIT twiddles W_1024^{m1 k0}, W_M^{m0 (k0 + 32 k1)}).
+//   * exchange 0 swaps the registers with lane bit 0 + wave bits: the one cross-wave
+//     exchange of the item (four rounds through LDS region A, workgroup barriers);
+//   * exchange 1 swaps the registers with lane bits 1-5 only, so it is WAVE-LOCAL: register
+//     bits 4 / 3 <-> lane bits 5 / 4 by v_permlane32_swap / v_permlane16_swap (one VALU
+//     instruction per register pair), register bits 0-2 <-> lane bits 1-3 through the wave's
+//     own 4 KiB slice of LDS in four balanced rounds -- no s_barrier;
+//   * the 8-bit frame is staged per WAVE: a wave's points of one half of the frame are 32
+//     pieces of 64 consecutive samples (128 B), which its own LDS-DMA brings into its own
+//     slices (half 0 -> region B right after its pre-stage, half 1 -> its region-A slice right
+//     after its exchange 1), so a wave waits for its own DMA only -- no item-start barrier.
+//
+// Between two passes of exchange 0 the waves run free: one wave's exchange 1 (LDS) and DMA
+// waits overlap the other waves' butterflies and dB epilogue on the same SIMD.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <type_traits>
+#include <vector>
+
+#include "fft_common.h"
+#include "fft_kernels.h"
+
+namespace rfa {
+namespace {
+
+constexpr int kM = 32768;            // points per residue item (N = 2 M)
+constexpr int kN = 65536;
+constexpr int kRow = 31;             // twiddle table row: t = 1 .. 31
+constexpr int kTw1 = 32 * kRow;      // T1[a][t - 1] = W_1024^{a t}
+constexpr int kTwLds = 2 * kTw1;     // + TB[k0][t - 1] = W_M^{t k0}
+constexpr int kPreA = kTwLds;        // blob only: W_N^c, c < 1024 (f32 residue 1)
+constexpr int kSliceA = 528;         // float2 per wave in region A: exchange-1 rounds (8 x 66) / staged half 1
+constexpr int kRegA = 16 * kSliceA;  // 8448: also the four-round exchange 0 (32 x 257 used)
+constexpr int kSliceB = 512;         // float2 per wave in region B: staged half 0 (4 KiB)
+constexpr int kRegB = 16 * kSliceB;
+constexpr int kLdsBytes = (kTwLds + kRegA + kRegB) * 8;  // 148,992 B
+static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
+
+#ifndef RFA_W64_X0R
+#define RFA_W64_X0R 4  // exchange-0 rounds: 4 through region A (half 0 staged early), 2 through A + B
+#endif
+
+// ---- wave-private staging: LDS-DMA of this wave's pieces x[64 w + 1024 t + half M], t < 32
+// (64 samples = 128 B of 8-bit IQ each) into its slice, piece t at slice + 128 t bytes.
+// Four wave instructions of 1 KiB (16 B per lane, lane-linear in LDS, per-lane source).
+// Inline asm like fft_wide.hip stage_frame: the builtin makes hipcc wait vmcnt(0) before
+// later LDS reads; completion is waited for explicitly at the start of the next item.
+__device__ __forceinline__ void stage_half(const uint8_t *frame, int half, float2 *slice, int w, int l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const rsrc_t rs = make_rsrc(frame, kN * 2);
+    const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)(uint8_t *)slice;
+    const int vo = half * (kM * 2) + w * 128 + (l >> 3) * 2048 + (l & 7) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(base + i * 1024), "v"(vo), "s"(rs), "s"(i * 16384)
+            : "memory");
+    }
+#else
+    (void)frame; (void)half; (void)slice; (void)w; (void)l;
+#endif
+}
+
+// v_permlane32_swap / v_permlane16_swap of both halves of a complex value: lanes 32-63
+// (odd 16-lane rows) of a trade places with lanes 0-31 (even rows) of b
+template <int BITS>
+__device__ __forceinline__ void lane_swap(float2 &a, float2 &b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (BITS == 32) {
+        const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+        const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+        a = make_float2(__uint_as_float(x[0]), __uint_as_float(y[0]));
+        b = make_float2(__uint_as_float(x[1]), __uint_as_float(y[1]));
+    } else {
+        const auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+        const auto y = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+        a = make_float2(__uint_as_float(x[0]), __uint_as_float(y[0]));
+        b = make_float2(__uint_as_float(x[1]), __uint_as_float(y[1]));
+    }
+#else
+    (void)a; (void)b;
+#endif
+}
+
+__device__ __forceinline__ void compiler_fence() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::: "memory");
+#endif
+}
+
+// ---- exchange 0 (cross-wave): registers k0 <-> (lane bit 0, wave bits); lane bits 1-5 (m0)
+// stay.  Round h: the WPR writer waves w / WPR == h store all 32 registers (one whole
+// k0-row of 64 lanes per instruction, contiguous), then every thread reads its RB registers
+// m1 = RB h + b.  Row pitch ROW + 1 float2: the odd / even reading lanes (k0 bit 0) land
+// two banks apart, conflict-free.
+template <int X0R>
+__device__ __forceinline__ void exchange0(float2 (&v)[32], float2 *buf, int l, int w) {
+    constexpr int WPR = 16 / X0R, RB = 32 / X0R, ROWP = WPR * 64 + 1;
+    const int k0 = (l & 1) | (w << 1);
+    auto wb = lds_opaque(buf + (w % WPR) * 64 + l);
+    auto rd = lds_opaque(buf + k0 * ROWP + (l & ~1));
+    float2 in[X0R][RB];
+#pragma unroll
+    for (int h = 0; h < X0R; h++) {
+        if (w / WPR == h) {
+#pragma unroll
+            for (int k = 0; k < 32; k++) wb[k * ROWP] = v[k];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int b = 0; b < RB; b++) in[h][b] = rd[(b >> 1) * 64 + (b & 1)];
+        lds_barrier();
+    }
+#pragma unroll
+    for (int m = 0; m < 32; m++) v[m] = in[m / RB][m % RB];
+}
+
+// ---- exchange 1 (wave-local): registers k1 <-> lane bits 1-5 (m0); lane bit 0 and the wave
+// bits (k0) stay.  Register bit 4 <-> lane bit 5 and bit 3 <-> lane bit 4 by permlane swaps,
+// then bits 0-2 <-> lane bits 1-3 through this wave's slice: round h, lane l stores its
+// registers 8h + a at a*66 + l and reads register 8h + b from lane (l & 0x31) | (b << 1),
+// slot (l >> 1) & 7.  LDS instructions of one wave execute in order, so the round needs no
+// barrier (the compiler fence keeps hipcc from moving the reads above the stores).
+__device__ __forceinline__ void exchange1(float2 (&v)[32], float2 *slice, int l) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) lane_swap<32>(v[j], v[j + 16]);
+#pragma unroll
+    for (int j = 0; j < 32; j++)
+        if ((j & 8) == 0) lane_swap<16>(v[j], v[j + 8]);
+    auto wb = lds_opaque(slice + l);
+    auto rd = lds_opaque(slice + ((l >> 1) & 7) * 66 + (l & 0x31));
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+#pragma unroll
+        for (int a = 0; a < 8; a++) wb[a * 66] = v[8 * h + a];
+        compiler_fence();
+#pragma unroll
+        for (int b = 0; b < 8; b++) v[8 * h + b] = lds_ld2(rd + 2 * b);
+        compiler_fence();
+    }
+}
+
+// ---- pre-stage (residue R of N = 2M): y_R[m] = W_N^{m R} (x[m] w[m] + (-1)^R x[m + M] w[m + M]),
+// m = col + 1024 t, t = register.  8/16-bit residue 1 folds W_N^m into the complex window
+// cw[m] = (w[m] W_N^m, -w[m + M] W_N^m) (fft_wide.hip prestage CW); f32 residue 1
+// uses W_N^{col} * W_64^t.  Staged input: this wave's samples at l0 / l1 + 64 t (halves 0 / 1).
+// Loads run one chunk of four points ahead of the arithmetic.
+template <int FMT, int R, bool STG, typename P>
+__device__ __forceinline__ void prestage(float2 (&v)[32], const float *window_il, const float4 *cw, float2 pa,
+                                         rsrc_t in_rs, int col, P l0, P l1) {
+    constexpr bool CW = R == 1 && FMT <= 2;
+    constexpr int SB = FMT == 4 ? 4 : ((FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8));
+    constexpr int C = 4, NCH = 32 / C;
+    const rsrc_t w_rs = CW ? make_rsrc(cw, kM * 16) : make_rsrc(window_il, kM * 8);
+    typename Raw<FMT>::T raw[2][C][2];
+    float win[2][C][CW ? 4 : 2];
+    auto issue = [&]<int c>() {
+        constexpr int s = c & 1;
+#pragma unroll
+        for (int q = 0; q < C; q++) {
+            const int t = c * C + q, mo = 1024 * t;
+            if constexpr (STG) {
+                raw[s][q][0] = l0[64 * t];
+                raw[s][q][1] = l1[64 * t];
+            } else {
+                raw[s][q][0] = buf_load_raw<FMT>(in_rs, col * SB, mo * SB, kN * 4);
+                raw[s][q][1] = buf_load_raw<FMT>(in_rs, col * SB, (mo + kM) * SB, kN * 4);
+            }
+            if constexpr (CW) {
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                const f4v x = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(w_rs, col * 16, mo * 16, 0));
+                win[s][q][0] = x.x;
+                win[s][q][1] = x.y;
+                win[s][q][2] = x.z;
+                win[s][q][3] = x.w;
+            } else {
+                const f2v x = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, col * 8, mo * 8, 0));
+                win[s][q][0] = x.x;
+                win[s][q][1] = x.y;
+            }
+        }
+    };
+    auto compute = [&]<int c>() {
+        constexpr int s = c & 1;
+        if constexpr (CW) {  // two points' cmac2 chains interleaved (fft_common.h cmac2x2)
+#pragma unroll
+            for (int q = 0; q < C; q += 2)
+                cmac2x2(v[c * C + q], convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
+                        convert_raw<FMT>(raw[s][q][1]), make_float2(win[s][q][2], win[s][q][3]), v[c * C + q + 1],
+                        convert_raw<FMT>(raw[s][q + 1][0]), make_float2(win[s][q + 1][0], win[s][q + 1][1]),
+                        convert_raw<FMT>(raw[s][q + 1][1]), make_float2(win[s][q + 1][2], win[s][q + 1][3]));
+        } else if constexpr (R == 0) {  // x[m] w[m] + x[m + M] w[m + M]: mul + fma
+#pragma unroll
+            for (int q = 0; q < C; q++) {
+                const f2v x0 = to_v(convert_raw<FMT>(raw[s][q][0])), x1 = to_v(convert_raw<FMT>(raw[s][q][1]));
+                v[c * C + q] = from_v(__builtin_elementwise_fma(x1, (f2v){win[s][q][1], win[s][q][1]}, x0 * win[s][q][0]));
+            }
+        } else {  // (x[m] w[m] - x[m + M] w[m + M]) * W_N^{col} * W_64^t
+            [&]<int... Qs>(std::integer_sequence<int, Qs...>) {
+                (
+                    [&] {
+                        constexpr int t = c * C + Qs;
+                        const f2v x0 = to_v(convert_raw<FMT>(raw[s][Qs][0])) * win[s][Qs][0];
+                        const f2v x1 = to_v(convert_raw<FMT>(raw[s][Qs][1])) * win[s][Qs][1];
+                        v[t] = w64<t & 63>(cmul(from_v(x0 - x1), pa));
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, C>{});
+        }
+    };
+    issue.template operator()<0>();
+    [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+        (
+            [&] {
+                if constexpr (Cs + 1 < NCH) issue.template operator()<Cs + 1>();
+                __builtin_amdgcn_sched_barrier(0);
+                compute.template operator()<Cs>();
+                __builtin_amdgcn_sched_barrier(0);
+            }(),
+            ...);
+    }(std::make_integer_sequence<int, NCH>{});
+}
+
+template <int FMT, bool STG, int X0R>
+__global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    for (int e = threadIdx.x; e < kTwLds; e += 1024) lds[e] = a.w64_tw[e];
+    float2 *ra = lds + kTwLds, *rb = ra + kRegA;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float2 *sa = ra + w * kSliceA, *sb = rb + w * kSliceB;  // this wave's slices
+    constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
+    using RawT = typename Raw<FMT>::T;
+    const int items = ((a.n_frames + 7) / 8) * 16;
+    // item u = (frame, residue): the two residues of a frame are items u, u + 8, i.e. blocks
+    // b and b + 8 of the persistent grid, one XCD (the second re-reads the frame from L2)
+    auto frame_of = [](int u) { return (u >> 4) * 8 + (u & 7); };
+    auto frame_ptr = [&](int f) { return a.in + (size_t)f * (size_t)a.frame_stride; };
+    __syncthreads();  // twiddle tables
+    if constexpr (STG) {
+        const int f0 = frame_of(blockIdx.x), l = threadIdx.x & 63;
+        if ((int)blockIdx.x < items && f0 < a.n_frames) {
+            stage_half(frame_ptr(f0), 0, sb, w, l);
+            stage_half(frame_ptr(f0), 1, sa, w, l);
+        }
+    }
+    const float db_off = -kDbPerLog2 * 32.0f;  // 2 log2 N
+    int pending_st = 0;  // stores issued after this wave's last staging DMA
+    for (int u = blockIdx.x; u < items; u += gridDim.x) {
+        const int un = u + gridDim.x, fn = frame_of(un);
+        const bool stage_next = STG && un < items && fn < a.n_frames;
+        const int frame = frame_of(u), r = (u >> 3) & 1;
+        const bool active = frame < a.n_frames;
+        int z;  // opaque zero: the per-item table reads are not hoisted out of the item loop
+        asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+        const float2 *t1 = lds + z, *tb = lds + kTw1 + z;
+        // lane index, opaque per item: the per-lane offsets below are rebuilt each item
+        // instead of being hoisted out of the item loop (and spilled)
+        int l = threadIdx.x & 63;
+        asm volatile("" : "+v"(l));
+        const int col = (l >> 1) + ((l & 1) << 5) + (w << 6);  // m0 + 32 m1 of this lane at pass 0
+        const int k0 = (l & 1) | (w << 1);                      // after exchange 0
+        const int k1 = l >> 1;                                  // after exchange 1
+        float2 v[32];
+        if constexpr (STG) {  // this wave's own pieces of the frame (younger: the epilogue stores)
+            if (pending_st >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+            else if (pending_st >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        {
+            const rsrc_t in_rs = make_rsrc(frame_ptr(active ? frame : 0), active ? (unsigned)(kN * BPS) : 0u);
+            auto run = [&](auto l0, auto l1) {
+                if (r == 0) {
+                    prestage<FMT, 0, STG>(v, a.window_il, a.window_cw, make_float2(0.f, 0.f), in_rs, col, l0, l1);
+                } else {
+                    float2 pa = make_float2(0.f, 0.f);
+                    if constexpr (FMT > 2) pa = buf_load_f32x2(make_rsrc(a.w64_tw + kPreA, 1024 * 8), col * 8, 0);
+                    prestage<FMT, 1, STG>(v, a.window_il, a.window_cw, pa, in_rs, col, l0, l1);
+                }
+            };
+            if constexpr (STG) {
+                const int q = (l >> 1) + ((l & 1) << 5);
+                run(lds_opaque(reinterpret_cast<RawT *>(sb) + q), lds_opaque(reinterpret_cast<RawT *>(sa) + q));
+            } else {
+                run((const RawT *)nullptr, (const RawT *)nullptr);
+            }
+        }
+        dft<32>(v);  // pass 0: m2 -> k0
+        if constexpr (STG && X0R == 4) {
+            if (stage_next) stage_half(frame_ptr(fn), 0, sb, w, l);
+        }
+        lds_barrier();  // every wave has read its staged pieces before exchange 0 reuses region A
+        exchange0<X0R>(v, ra, l, w);
+        // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1
+        {
+            const float2 *row = t1 + k0 * kRow - 1;
+            v[1] = cmul(v[1], lds_ld2(row + 1));
+#pragma unroll
+            for (int t = 2; t < 32; t += 2) cmul2(v[t], lds_ld2(row + t), v[t + 1], lds_ld2(row + t + 1));
+        }
+        dft<32>(v);
+        if constexpr (STG && X0R == 2) {
+            if (stage_next) stage_half(frame_ptr(fn), 0, sb, w, l);
+        }
+        exchange1(v, sa, l);
+        if constexpr (STG) {
+            if (stage_next) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's slice reads are done
+                stage_half(frame_ptr(fn), 1, sa, w, l);
+            }
+        }
+        // pass 2: twiddle W_M^{m0 (k0 + 32 k1)} = T1[k1][m0] * TB[k0][m0], DFT over m0 -> k2
+        {
+            const float2 *pa_ = t1 + k1 * kRow - 1, *pb_ = tb + k0 * kRow - 1;
+            const float2 w1 = cmul(lds_ld2(pa_ + 1), lds_ld2(pb_ + 1));
+            v[1] = cmul(v[1], w1);
+#pragma unroll
+            for (int t = 2; t < 32; t += 2) {
+                float2 w0 = lds_ld2(pa_ + t), w2 = lds_ld2(pa_ + t + 1);
+                cmul2(w0, lds_ld2(pb_ + t), w2, lds_ld2(pb_ + t + 1));
+                cmul2(v[t], w0, v[t + 1], w2);
+            }
+        }
+        dft<32>(v);
+        pending_st = 0;
+        if (!active) continue;
+        // ---- epilogue: register t holds sub-bin k0 + 32 k1 + 1024 t = full bin 2 (...) + r; the
+        // fft-shift (nativedsp.cpp:77) flips t's bit 4: t' = t ^ 16
+        const bool to_ring = a.ring && frame >= a.ring_first;
+        int rr = 0;
+        if (to_ring) {
+            rr = (a.ring_base - frame) % a.ring_rows;
+            if (rr < 0) rr += a.ring_rows;
+        }
+        const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * kN : nullptr, a.rows ? kN * 4 : 0);
+        // ring (kRingTile2): block r, thread (w, l)'s registers t' = 4j .. 4j+3 as one 16-B store
+        const rsrc_t ring_rs =
+            make_rsrc(to_ring ? a.ring + (size_t)rr * kN + (size_t)r * kM : nullptr, to_ring ? kM * 4 : 0);
+        const int tvo = (w * 2048 + l * 4) * 4;
+        const int rvo = (2 * (k0 + 32 * k1) + r) * 4;  // natural row: bin 2 (k0 + 32 k1 + 1024 t') + r
+        auto store = [&](auto rows_c, auto ring_c) {
+            [&]<int... Js>(std::integer_sequence<int, Js...>) {
+                (
+                    [&] {
+                        constexpr int j = Js;
+                        float d[4];
+                        [&]<int... Es>(std::integer_sequence<int, Es...>) {
+                            (
+                                [&] {
+                                    constexpr int tp = 4 * j + Es;
+                                    d[Es] = db_unscaled(v[tp ^ 16], db_off);  // nativedsp.cpp:73-78
+                                    if constexpr (decltype(rows_c)::value) buf_store_f32_c<2048 * tp * 4>(d[Es], row_rs, rvo);
+                                }(),
+                                ...);
+                        }(std::make_integer_sequence<int, 4>{});
+                        if constexpr (decltype(ring_c)::value) buf_store_f32x4(d[0], d[1], d[2], d[3], ring_rs, tvo, j * 1024);
+                    }(),
+                    ...);
+            }(std::make_integer_sequence<int, 8>{});
+        };
+        using T_ = std::true_type;
+        using F_ = std::false_type;
+        if (a.rows && to_ring) store(T_{}, T_{});
+        else if (a.rows) store(T_{}, F_{});
+        else if (to_ring) store(F_{}, T_{});
+        pending_st = (a.rows ? 32 : 0) + (to_ring ? 8 : 0);
+    }
+}
+
+template <int FMT, bool STG, int X0R>
+hipError_t launch64_one(const FftLaunch &a) {
+    auto kern = &fft64_kernel<FMT, STG, X0R>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytes);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    const int items = ((a.n_frames + 7) / 8) * 16;
+    if (items <= 0) return hipSuccess;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    }
+    const int blocks = std::min(items, cus);  // persistent: one 1024-thread workgroup per CU
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(1024), kLdsBytes, a.stream, a);
+    return hipGetLastError();
+}
+
+template <int X0R>
+hipError_t launch64_x(const FftLaunch &a) {
+    const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
+    switch (a.fmt) {
+    case 0: return stg ? launch64_one<0, true, X0R>(a) : launch64_one<0, false, X0R>(a);
+    case 1: return stg ? launch64_one<1, true, X0R>(a) : launch64_one<1, false, X0R>(a);
+    case 2: return launch64_one<2, false, X0R>(a);
+    case 3: return launch64_one<3, false, X0R>(a);
+    case 4: return launch64_one<4, false, X0R>(a);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+// Twiddle blob (exact, correctly rounded from double): T1[a][t-1] = W_1024^{a t},
+// TB[k0][t-1] = W_32768^{t k0} (a, k0 < 32, t = 1..31), then W_65536^c (c < 1024).
+std::vector<float2> w64_twiddles() {
+    auto w = [](double num, double den) {
+        const double ang = -2.0 * M_PI * num / den;
+        return make_float2((float)std::cos(ang), (float)std::sin(ang));
+    };
+    std::vector<float2> blob;
+    for (int i = 0; i < 32; i++)
+        for (int t = 1; t < 32; t++) blob.push_back(w((double)i * t, 1024.0));
+    for (int i = 0; i < 32; i++)
+        for (int t = 1; t < 32; t++) blob.push_back(w((double)t * i, (double)kM));
+    for (int c = 0; c < 1024; c++) blob.push_back(w((double)c, (double)kN));
+    return blob;
+}
+
+hipError_t launch_fft64(const FftLaunch &a) {
+    if (a.logn != 16 || a.complex_out || !a.w64_tw || !a.window_il) return hipErrorInvalidValue;
+    if (a.fmt <= 2 && !a.window_cw) return hipErrorInvalidValue;
+    if (a.ring && (a.ring_logrs != (1 | kRingTile2) || a.ring_rows <= 0)) return hipErrorInvalidValue;
+#ifdef RFA_AB_BUILD
+    if (const char *x = std::getenv("RFA_W64_X0R"); x && std::atoi(x) == 2) return launch64_x<2>(a);
+#endif
+    return launch64_x<RFA_W64_X0R>(a);
+}
+
+}  // namespace rfa

@@ -15,45 +15,71 @@
 
 namespace {
 
+// The legacy symbols share a small cache of setups keyed by (N, input format, window),
+// least recently used out: alternating performFFT (f32, no window), performFFTAndLogMag and
+// processIqBytesNative (raw bytes, Blackman) keeps each one's handle -- no table rebuild,
+// and the framing mode's partial frame stays pending on its handle between calls.
+constexpr int kCacheSlots = 4;
+struct Setup {
+    rfa_handle *h = nullptr;
+    int n = 0, fmt = -1, win = -1;
+    unsigned long long used = 0;
+};
 std::mutex g_mu;
-rfa_handle *g_handle = nullptr;  // the shim's cached "setup"
-int g_n = 0, g_fmt = -1, g_win = -1;
+Setup g_cache[kCacheSlots];
+unsigned long long g_tick = 0;
+int g_status = RFA_OK;  // status of the last legacy call (rfa_jni_last_status)
 
 rfa_handle *handle_for(int n, int fmt, int window) {
-    if (g_handle && g_n == n && g_fmt == fmt && g_win == window) return g_handle;
-    if (g_handle) rfa_destroy(g_handle);
-    g_handle = nullptr;
+    Setup *victim = &g_cache[0];
+    for (Setup &s : g_cache) {
+        if (s.h && s.n == n && s.fmt == fmt && s.win == window) {
+            s.used = ++g_tick;
+            return s.h;
+        }
+        if (!s.h || (victim->h && s.used < victim->used)) victim = &s;
+    }
+    if (victim->h) rfa_destroy(victim->h);
+    *victim = Setup();
     rfa_config c;
     rfa_default_config(&c);
     c.fft_size = n;
     c.input_format = fmt;
     c.window = window;
     c.ring_rows = 0;
-    if (rfa_create(&c, &g_handle) != RFA_OK) {
-        g_handle = nullptr;
-        g_n = 0;
-        return nullptr;
-    }
-    g_n = n;
-    g_fmt = fmt;
-    g_win = window;
-    return g_handle;
+    rfa_handle *h = nullptr;
+    g_status = rfa_create(&c, &h);  // e.g. RFA_ERR_UNSUPPORTED for a length pffft takes and librfa does not
+    if (g_status != RFA_OK) return nullptr;
+    victim->h = h;
+    victim->n = n;
+    victim->fmt = fmt;
+    victim->win = window;
+    victim->used = ++g_tick;
+    return h;
 }
 
 }  // namespace
 
 extern "C" {
 
+JNIEXPORT int rfa_jni_abi_version(void) { return RFA_JNI_ABI_VERSION; }
+
+JNIEXPORT int rfa_jni_last_status(void) {
+    std::lock_guard<std::mutex> lock(g_mu);
+    return g_status;
+}
+
 JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFT(JNIEnv *env, jobject, jfloatArray input,
                                                                           jfloatArray output) {
     const jsize length = (*env)->GetArrayLength(env, input);
-    if (length <= 0 || (length & 1)) return;
     std::lock_guard<std::mutex> lock(g_mu);
+    g_status = RFA_ERR_UNSUPPORTED;
+    if (length <= 0 || (length & 1)) return;
     rfa_handle *h = handle_for(length / 2, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE);
     if (!h) return;
     std::vector<float> in(length), out(length);
     (*env)->GetFloatArrayRegion(env, input, 0, length, in.data());
-    if (rfa_fft_ordered(h, in.data(), out.data(), (size_t)length / 2) != RFA_OK) return;
+    if ((g_status = rfa_fft_ordered(h, in.data(), out.data(), (size_t)length / 2)) != RFA_OK) return;
     (*env)->SetFloatArrayRegion(env, output, 0, length, out.data());
 }
 
@@ -61,28 +87,33 @@ JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFTAndLogMa
                                                                                    jfloatArray input,
                                                                                    jfloatArray output) {
     const jsize length = (*env)->GetArrayLength(env, input);
+    std::lock_guard<std::mutex> lock(g_mu);
+    g_status = RFA_ERR_UNSUPPORTED;
     if (length <= 0 || (length & 1)) return;
     const jsize out_len = length / 2;
-    std::lock_guard<std::mutex> lock(g_mu);
     rfa_handle *h = handle_for(out_len, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE);
     if (!h) return;
     std::vector<float> in(length), mag(out_len);
     (*env)->GetFloatArrayRegion(env, input, 0, length, in.data());
-    if (rfa_fft_logmag_interleaved(h, in.data(), mag.data(), (size_t)out_len) != RFA_OK) return;
+    if ((g_status = rfa_fft_logmag_interleaved(h, in.data(), mag.data(), (size_t)out_len)) != RFA_OK) return;
     (*env)->SetFloatArrayRegion(env, output, 0, out_len, mag.data());
 }
 
 JNIEXPORT jboolean JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performWindowedFftAndReturnMagNative(
     JNIEnv *env, jobject, jfloatArray re, jfloatArray im, jfloatArray mag_out) {
     const jsize n = (*env)->GetArrayLength(env, re);
-    if ((*env)->GetArrayLength(env, im) != n || (*env)->GetArrayLength(env, mag_out) != n) return JNI_FALSE;
+    if ((*env)->GetArrayLength(env, im) != n || (*env)->GetArrayLength(env, mag_out) != n) {
+        std::lock_guard<std::mutex> lock(g_mu);
+        g_status = RFA_ERR_SIZE;
+        return JNI_FALSE;
+    }
     std::lock_guard<std::mutex> lock(g_mu);
     rfa_handle *h = handle_for(n, RFA_IN_F32_PLANAR, RFA_WINDOW_BLACKMAN);
     if (!h) return JNI_FALSE;
     std::vector<float> r(n), i(n), m(n);
     (*env)->GetFloatArrayRegion(env, re, 0, n, r.data());
     (*env)->GetFloatArrayRegion(env, im, 0, n, i.data());
-    if (rfa_windowed_fft_mag_planar(h, r.data(), i.data(), m.data(), (size_t)n) != RFA_OK) return JNI_FALSE;
+    if ((g_status = rfa_windowed_fft_mag_planar(h, r.data(), i.data(), m.data(), (size_t)n)) != RFA_OK) return JNI_FALSE;
     (*env)->SetFloatArrayRegion(env, mag_out, 0, n, m.data());
     return JNI_TRUE;
 }
@@ -97,6 +128,7 @@ JNIEXPORT jint JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_processIqBytesNati
     std::lock_guard<std::mutex> lock(g_mu);
     rfa_handle *h = handle_for(fft_size, format, RFA_WINDOW_BLACKMAN);
     if (!h) return -1;
+    g_status = RFA_OK;
     std::vector<jbyte> in((size_t)bytes);
     if (bytes) (*env)->GetByteArrayRegion(env, packet, 0, bytes, in.data());
     if (frame_stride == 0) {

@@ -53,6 +53,16 @@ def test_library_embeds_gfx950_code_object(lib):
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data
 
 
+def test_jni_abi_version_and_framing_sentinel(lib):
+    """rfa_jni.h RFA_JNI_ABI_VERSION 2: frame_stride 0 of the raw-packet natives is the
+    reference's packet framing; a caller built against version 1 (0 = dense
+    batch) can detect the change at load time.  No legacy call yet: last status RFA_OK."""
+    text = open(os.path.join(INCLUDE, "rfa_jni.h")).read()
+    ver = int(re.search(r"#define RFA_JNI_ABI_VERSION (\d+)", text).group(1))
+    assert ver == 2 and lib.rfa_jni_abi_version() == ver
+    assert lib.rfa_jni_last_status() == 0
+
+
 def test_status_strings_and_defaults(lib):
     from rfanalyzer_amd._lib import RfaConfig
     assert lib.rfa_abi_version() == 1

@@ -158,3 +158,67 @@ def test_process_iq_bytes_native_fills_across_calls(rfa):
     # a mag_out shorter than one row is an error, not a silent partial copy
     assert fn(jenv.env, None, jenv.new_array(np.frombuffer(packets[0], np.int8).copy()), 0, n, 0,
               jenv.new_array(np.zeros(n - 1, np.float32))) == -1
+
+
+def test_legacy_calls_alternate_without_losing_the_partial_frame(rfa):
+    """The legacy symbols share an LRU cache of setups keyed by (N, format, window)
+    (jni_shim.cpp handle_for): performFFT (f32, no window) between the packets of
+    processIqBytesNative's framing mode (s8, Blackman) neither rebuilds that setup nor
+    drops its partial frame -- every row of the reference framing arrives, and every
+    performFFT result equals the reference's pffft."""
+    n, pkt = 8192, 6000
+    raw = signals.frames_bytes(n, 6, "s8", 11, tones=((0.21, 0.5),), noise=0.03)
+    jenv = MockJNIEnv()
+    fn = getattr(rfa.lib(), _P + "processIqBytesNative")
+    fn.restype = _I32
+    fn.argtypes = [_V, _V, _V, _I32, _I32, _I32, _V]
+    fft = getattr(rfa.lib(), _P + "performFFT")
+    fft.restype = None
+    fft.argtypes = [_V, _V, _V, _V]
+    status = rfa.lib().rfa_jni_last_status
+    status.restype = _I32
+    packets = [raw[i:i + pkt] for i in range(0, len(raw) - pkt + 1, pkt)]
+    frames = processor.scheduler_frames([(b, 0, 1) for b in packets], n, 2)
+    rng = np.random.default_rng(5)
+    rows = []
+    for k, b in enumerate(packets):
+        out = np.zeros(n, np.float32)
+        got = fn(jenv.env, None, jenv.new_array(np.frombuffer(b, np.int8).copy()), 0, n, 0, jenv.new_array(out))
+        assert got in (0, 1) and status() == 0
+        if got:
+            rows.append(out)
+        m = (1024, 2048)[k % 2]  # two more setups in the cache between the packets
+        x = rng.standard_normal(2 * m).astype(np.float32)
+        y = np.zeros(2 * m, np.float32)
+        fft(jenv.env, None, jenv.new_array(x), jenv.new_array(y))
+        assert status() == 0
+        if oracle.ref_available():
+            ref = oracle.ref_fft_ordered(x)
+            assert np.abs(y - ref).max() / np.abs(ref).max() < 1e-5
+    assert len(rows) == len(frames)
+    exp = np.stack([oracle.spectrum_rows(f[0], oracle.IN_S8, n, 1, None, oracle.WIN_BLACKMAN)[0] for f in frames])
+    assert gu.db_diff(np.stack(rows), exp) <= gu.DB_TOL
+
+
+@pytest.mark.parametrize("m", [48, 480, 16, 32])
+def test_legacy_unsupported_length_reports_status(rfa, m):
+    """Lengths the reference's pffft takes (a multiple of 16 with factors 2, 3, 5:
+    pffft.c:1236-1247) but librfa does not (powers of two from 64): the void legacy
+    symbol leaves its output untouched and rfa_jni_last_status() says
+    RFA_ERR_UNSUPPORTED; the next supported call resets it to RFA_OK."""
+    jenv = MockJNIEnv()
+    status = rfa.lib().rfa_jni_last_status
+    status.restype = _I32
+    for name in ("performFFT", "performFFTAndLogMag"):
+        fn = getattr(rfa.lib(), _P + name)
+        fn.restype = None
+        fn.argtypes = [_V, _V, _V, _V]
+        x = np.ones(2 * m, np.float32)
+        out = np.full(2 * m, 7.0, np.float32)
+        arr = jenv.new_array(out)
+        fn(jenv.env, None, jenv.new_array(x), arr)
+        assert status() == -3  # RFA_ERR_UNSUPPORTED
+        assert np.all(out == 7.0)
+        good = np.zeros(2 * 64, np.float32)
+        fn(jenv.env, None, jenv.new_array(np.ones(2 * 64, np.float32)), jenv.new_array(good))
+        assert status() == 0
