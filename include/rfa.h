@@ -133,15 +133,17 @@ RFA_API int rfa_synchronize(rfa_handle *h);
 RFA_API int rfa_process(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 RFA_API int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t frame_stride_bytes, float *rows);
 
-/* Multi-batch enqueue: exactly n_batches consecutive rfa_process calls (ring,
- * peaks, EMA and channel means advance batch after batch), batch b reading
+/* Multi-batch enqueue: the result of n_batches consecutive rfa_process calls (ring,
+ * peaks, EMA and channel means advance batch after batch; ring rows, peaks and
+ * channel means identical, the EMA equal to fp32 rounding -- the packed launch's
+ * chunked scan associates the recursion differently), batch b reading
  * frames_per_batch frames at in + b * batch_stride_bytes + f * frame_stride_bytes
  * and writing its rows (if rows != NULL) at rows + b * frames_per_batch * N.
  * When the batches are packed (batch_stride_bytes == frames_per_batch * frame
  * stride) the whole run is ONE kernel launch, so small batches (BASELINE
  * config 4: 256 x 8192 points) stop paying a host call + launch each.
- * Device pointers, asynchronous on the handle stream; channel means are those
- * of the last batch. */
+ * Device pointers, asynchronous on the handle stream; rfa_get_channel_means then
+ * returns the last batch's frames_per_batch means, in either form. */
 RFA_API int rfa_process_batches(rfa_handle *h, const void *in, size_t n_batches, size_t batch_stride_bytes,
                                 size_t frames_per_batch, size_t frame_stride_bytes, float *rows);
 
@@ -157,6 +159,9 @@ RFA_API int rfa_process_batches(rfa_handle *h, const void *in, size_t n_batches,
  * ceil(N / P) packets when P < N (e.g. RTL-SDR's 16 KiB = 8192-sample packets,
  * RtlsdrSource.java:112, at the default N = 16384).  *frames = 1 when a frame
  * was processed (its row copied to row_out, N floats, unless NULL), else 0.
+ * Only the completing packet's frequency / sample_rate are used, so only its
+ * sample_rate must be > 0 (else RFA_ERR_INVALID and the frame is dropped); a
+ * packet that only partly fills the frame is always accepted.
  * Synchronous.  RFA_ERR_UNSUPPORTED for RFA_IN_F32_PLANAR.  rfa_reset_state and
  * rfa_set_fft_size discard a partial frame (Scheduler.kt:259-260);
  * rfa_pending_samples reports how many samples it holds. */
@@ -201,7 +206,9 @@ RFA_API int rfa_set_fft_size(rfa_handle *h, int32_t fft_size);
  * clamped to [0, N], f0 = frequency - sampleRate / 2 (the tuning of
  * rfa_set_tuning).  start_frequency == end_frequency disables it.  The sum is a
  * deterministic parallel reduction: equal to the reference's sequential fp32 loop
- * (:150-152) over the same row to the rounding of the sum.
+ * (:150-152) over the same row to the rounding of the sum -- so a
+ * frame whose mean lies within that rounding of the squelch threshold can fall on
+ * the other side of it than in the reference.
  * rfa_get_channel_means copies the last batch's means in frame order
  * (synchronises); *count = 0 when the channel range is empty. */
 RFA_API int rfa_set_channel(rfa_handle *h, int64_t start_frequency, int64_t end_frequency);

@@ -84,6 +84,7 @@ struct rfa_handle {
     int64_t view_frequency = 0, view_sample_rate = 0;
     float view_min_db = 0.f, view_max_db = 0.f;
     size_t chan_count = 0;
+    size_t chan_offset = 0;           // first frame of the means rfa_get_channel_means returns (packed batches: the last batch)
     int64_t last_frequency = 0, last_sample_rate = 0;
     // rfa_push_packet: the partial SamplePacket Scheduler.run fills across packets
     rfa::PacketFramer framer;
@@ -694,6 +695,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     }
     const bool need_chan = chan_last > chan_first;
     h->chan_count = 0;
+    h->chan_offset = 0;
     // state and channel means need the rows of the whole batch: use the caller's,
     // else the ring when every frame lands there, else a staging buffer
     float *state_rows = rows;
@@ -787,7 +789,12 @@ int rfa_process_batches(rfa_handle *h, const void *in, size_t n_batches, size_t 
         // packed: one batch of n_batches * frames_per_batch frames is the same frame stream
         // (the ring and the peak / EMA recursion see the frames in the same order)
         if (n_batches > (size_t)0x7fffffff / frames_per_batch) return fail(h, RFA_ERR_INVALID, "too many frames");
-        return process_impl(h, in, n_batches * frames_per_batch, stride, rows, h->d_window, h->cfg.input_format);
+        rc = process_impl(h, in, n_batches * frames_per_batch, stride, rows, h->d_window, h->cfg.input_format);
+        if (!rc && h->chan_count) {  // the channel means of the last batch, as after consecutive calls
+            h->chan_offset = (n_batches - 1) * frames_per_batch;
+            h->chan_count = frames_per_batch;
+        }
+        return rc;
     }
     for (size_t b = 0; b < n_batches; b++) {
         rc = process_impl(h, static_cast<const uint8_t *>(in) + b * batch_stride_bytes, frames_per_batch, stride,
@@ -825,11 +832,17 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
 
 int rfa_push_packet(rfa_handle *h, const void *packet, size_t packet_bytes, int64_t frequency, int64_t sample_rate,
                     float *row_out, int32_t *frames) {
-    if (!h || !frames || (!packet && packet_bytes) || sample_rate <= 0) return RFA_ERR_INVALID;
+    if (!h || !frames || (!packet && packet_bytes)) return RFA_ERR_INVALID;
     *frames = 0;
     if (h->cfg.input_format == RFA_IN_F32_PLANAR)
         return fail(h, RFA_ERR_UNSUPPORTED, "packet framing needs an interleaved sample format");
     if (!h->framer.push(packet, packet_bytes)) return RFA_OK;  // the frame waits for more packets
+    // only the completing packet's tuning is used (Signed8BitIQConverter.java:95-97), so only
+    // its sample rate must be valid; the frame is dropped with it
+    if (sample_rate <= 0) {
+        h->framer.clear();
+        return fail(h, RFA_ERR_INVALID, "rfa_push_packet: sample_rate <= 0 on the packet completing a frame");
+    }
     // complete: the tuning of the packet that completed it (Signed8BitIQConverter.java:95-96),
     // then one frame through ring / peaks / EMA / channel mean (FftProcessor.kt:125-245)
     int rc = rfa_set_tuning(h, frequency, sample_rate);
@@ -1040,7 +1053,7 @@ int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, size_t *co
     int rc = set_device(h);
     if (rc) return rc;
     const size_t k = std::min(capacity, h->chan_count);
-    if (k) HIPCHK(h, hipMemcpyAsync(out, h->d_chan, k * sizeof(float), hipMemcpyDeviceToHost, h->stream));
+    if (k) HIPCHK(h, hipMemcpyAsync(out, h->d_chan + h->chan_offset, k * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     *count = h->chan_count;
     return RFA_OK;

@@ -374,11 +374,7 @@ __device__ __forceinline__ float2 tw(const float2 *twc, const float2 *twf, int s
 // operations (lgkmcnt) but NOT for its global loads (vmcnt), so the next
 // frame's prefetched samples stay in flight across the FFT passes.
 // (__syncthreads() would emit vmcnt(0) and drain them.)
-#ifdef RFA_SYNCTHREADS_BARRIER
-__device__ __forceinline__ void lds_barrier() { __syncthreads(); }
-#else
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-#endif
 
 // LDS pointer the compiler cannot see through: per-thread LDS bases built
 // inside a work item are then not hoisted out of the item loop (and spilled).
@@ -535,9 +531,6 @@ __device__ __forceinline__ void buf_store_f32_c(float x, rsrc_t rs, int voff) {
     (void)x; (void)rs; (void)voff;
 #endif
 }
-#ifndef RFA_X4_POLICY
-#define RFA_X4_POLICY ""  // cache policy of the 16-B ring stores (A/B builds: "nt", "sc1")
-#endif
 // 16-B store.  Inline asm with a trailing s_nop: a VALU write to the data VGPRs of a
 // just-issued buffer store of more than 64 bits needs a wait state, and hipcc (ROCm
 // 7.2, gfx950) let the next v_pk_fma overwrite them back to back -- the last lanes of
@@ -548,7 +541,7 @@ __device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float
     i32x4 v = {__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), __builtin_bit_cast(int, c),
                __builtin_bit_cast(int, d)};
 #if defined(__HIP_DEVICE_COMPILE__)
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen " RFA_X4_POLICY "\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
                  "s"(soff)
                  : "memory");
 #else

@@ -541,9 +541,6 @@ __global__ void state_combine_kernel(StateLaunch a, int chunks) {
 // all CH chunks of frames; the chunk summaries meet in LDS and the block folds
 // them in frame order into peaks / EMA (same algebra as state_combine_kernel),
 // so no summary buffer round trip and no second launch.
-#ifndef RFA_STATE_UNROLL
-#define RFA_STATE_UNROLL 4  // frames in flight per thread (A/B builds)
-#endif
 template <int CH>
 __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chunk_len) {
     constexpr int TPC = 256 / CH, BPB = 4 * TPC;  // threads per chunk, bins per block
@@ -557,7 +554,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
 #pragma unroll
     for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
     float am = 1.0f;
-#pragma unroll RFA_STATE_UNROLL
+#pragma unroll 4  // frames in flight per thread (profiles/r02c/state_unroll_ab.txt)
     for (int f = f0; f < f1; f++) {
         const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};

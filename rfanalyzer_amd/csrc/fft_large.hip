@@ -32,12 +32,6 @@
 
 namespace rfa {
 
-#ifndef RFA_DIF_SMEM
-#define RFA_DIF_SMEM 1  // pipelined front kernel: C twiddle factors by scalar loads (A/B builds: 0)
-#endif
-#ifndef RFA_DIF_ABL
-#define RFA_DIF_ABL 0  // ablations (A/B builds only): 1 no z stores, 2 no twiddles
-#endif
 template <int S, int FMT>
 __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     constexpr int M = 1 << kDitLogM, n = S * M;
@@ -107,7 +101,7 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     // twiddle carries C's rounding and one add instead of a full product's.  Chunks
     // of 8 (scheduling barriers) keep the delta loads from all being live at once.
 #pragma unroll
-    for (int s0 = 0; s0 < S && !(RFA_DIF_ABL & 2); s0 += 8) {
+    for (int s0 = 0; s0 < S; s0 += 8) {
         float2 d[8];
 #pragma unroll
         for (int s = s0; s < s0 + 8 && s < S; s++) d[s - s0] = a.tw_d[s * 128 + klo];
@@ -120,10 +114,7 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     }
     const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
 #pragma unroll
-    for (int s = 0; s < S; s++) {
-        if constexpr (RFA_DIF_ABL & 1) asm volatile("" ::"v"(v[s].x), "v"(v[s].y));
-        else buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
-    }
+    for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
 }
 
 // 8-bit formats, persistent and pipelined: block b owns the 256 columns
@@ -189,7 +180,8 @@ __global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int gr
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave has read the tile
         if (f + groups < a.n_frames) stage(f + groups);
         dft<S>(v);
-        if constexpr (RFA_DIF_SMEM) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel; C in SGPRs
+        {  // W_N^{m s} = C (1 + delta), as dif_front_kernel; C in SGPRs (scalar loads,
+           // profiles/r03/dif_front_smem_ab.txt)
             {
                 const float2 c = c_at(mc + khi), corr = cmul(c, dtab[128 + klo]);
                 v[1] = cmul(v[1], make_float2(c.x + corr.x, c.y + corr.y));
@@ -198,12 +190,6 @@ __global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int gr
             for (int s = 2; s < S; s += 2)
                 twiddle_cd2(v[s], dtab[s * 128 + klo], c_at(s * mc + khi), v[s + 1], dtab[(s + 1) * 128 + klo],
                             c_at((s + 1) * mc + khi));
-        } else {
-#pragma unroll
-            for (int s = 1; s < S; s++) {  // W_N^{m s} = C (1 + delta), as dif_front_kernel
-                const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, dtab[s * 128 + klo]);
-                v[s] = cmul(v[s], make_float2(c.x + corr.x, c.y + corr.y));
-            }
         }
         const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
 #pragma unroll

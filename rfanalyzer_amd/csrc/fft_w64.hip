@@ -126,7 +126,7 @@ __device__ __forceinline__ void exchange0(float2 (&v)[32], float2 *buf, int l, i
         }
         lds_barrier();
 #pragma unroll
-        for (int b = 0; b < RB; b++) in[h][b] = rd[(b >> 1) * 64 + (b & 1)];
+        for (int b = 0; b < RB; b++) in[h][b] = lds_ld2(rd + (b >> 1) * 64 + (b & 1));  // unfused ds_read_b64
         lds_barrier();
     }
 #pragma unroll
@@ -239,7 +239,11 @@ __device__ __forceinline__ void prestage(float2 (&v)[32], const float *window_il
     }(std::make_integer_sequence<int, NCH>{});
 }
 
-template <int FMT, bool STG, int X0R>
+// DIAG 32 (A/B builds only): s_memrealtime stamps of every wave's phases, lane 0 of each
+// wave into a.stamps[block][item < 4][wave][8] (engine RFA_STAMPS_FILE, scripts/stamps_w64.py):
+// 0 item start, 1 own DMA landed, 2 pass 0 done, 3 exchange-0 entry barrier passed,
+// 4 exchange 0 done, 5 pass 1 done, 6 exchange 1 (+ DMA issue) done, 7 pass 2 + epilogue done
+template <int FMT, bool STG, int X0R, int DIAG = 0>
 __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     for (int e = threadIdx.x; e < kTwLds; e += 1024) lds[e] = a.w64_tw[e];
@@ -263,7 +267,17 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
     }
     const float db_off = -kDbPerLog2 * 32.0f;  // 2 log2 N
     int pending_st = 0;  // stores issued after this wave's last staging DMA
-    for (int u = blockIdx.x; u < items; u += gridDim.x) {
+    int it = 0;
+    auto stamp = [&](int k) {
+        if constexpr (DIAG & 32) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            int wi = (int)(threadIdx.x >> 6);  // per-lane (VGPR) index math, kept opaque
+            asm volatile("" : "+v"(wi));
+            if ((threadIdx.x & 63) == 0 && it < 4) a.stamps[(((size_t)blockIdx.x * 4 + it) * 16 + wi) * 8 + k] = t;
+        }
+    };
+    for (int u = blockIdx.x; u < items; u += gridDim.x, it++) {
+        stamp(0);
         const int un = u + gridDim.x, fn = frame_of(un);
         const bool stage_next = STG && un < items && fn < a.n_frames;
         const int frame = frame_of(u), r = (u >> 3) & 1;
@@ -284,6 +298,7 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
             else if (pending_st >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        stamp(1);
         {
             const rsrc_t in_rs = make_rsrc(frame_ptr(active ? frame : 0), active ? (unsigned)(kN * BPS) : 0u);
             auto run = [&](auto l0, auto l1) {
@@ -303,11 +318,14 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
             }
         }
         dft<32>(v);  // pass 0: m2 -> k0
+        stamp(2);
         if constexpr (STG && X0R == 4) {
             if (stage_next) stage_half(frame_ptr(fn), 0, sb, w, l);
         }
         lds_barrier();  // every wave has read its staged pieces before exchange 0 reuses region A
+        stamp(3);
         exchange0<X0R>(v, ra, l, w);
+        stamp(4);
         // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1
         {
             const float2 *row = t1 + k0 * kRow - 1;
@@ -316,6 +334,7 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
             for (int t = 2; t < 32; t += 2) cmul2(v[t], lds_ld2(row + t), v[t + 1], lds_ld2(row + t + 1));
         }
         dft<32>(v);
+        stamp(5);
         if constexpr (STG && X0R == 2) {
             if (stage_next) stage_half(frame_ptr(fn), 0, sb, w, l);
         }
@@ -326,6 +345,7 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
                 stage_half(frame_ptr(fn), 1, sa, w, l);
             }
         }
+        stamp(6);
         // pass 2: twiddle W_M^{m0 (k0 + 32 k1)} = T1[k1][m0] * TB[k0][m0], DFT over m0 -> k2
         {
             const float2 *pa_ = t1 + k1 * kRow - 1, *pb_ = tb + k0 * kRow - 1;
@@ -381,12 +401,13 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
         else if (a.rows) store(T_{}, F_{});
         else if (to_ring) store(F_{}, T_{});
         pending_st = (a.rows ? 32 : 0) + (to_ring ? 8 : 0);
+        stamp(7);
     }
 }
 
-template <int FMT, bool STG, int X0R>
+template <int FMT, bool STG, int X0R, int DIAG = 0>
 hipError_t launch64_one(const FftLaunch &a) {
-    auto kern = &fft64_kernel<FMT, STG, X0R>;
+    auto kern = &fft64_kernel<FMT, STG, X0R, DIAG>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -410,6 +431,12 @@ hipError_t launch64_one(const FftLaunch &a) {
 template <int X0R>
 hipError_t launch64_x(const FftLaunch &a) {
     const bool stg = a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0;
+#ifdef RFA_AB_BUILD
+    if ((a.diag & 32) && a.stamps) {  // phase stamps (profiling only): staged s8
+        if (a.fmt != 0 || !stg) return hipErrorInvalidValue;
+        return launch64_one<0, true, X0R, 32>(a);
+    }
+#endif
     switch (a.fmt) {
     case 0: return stg ? launch64_one<0, true, X0R>(a) : launch64_one<0, false, X0R>(a);
     case 1: return stg ? launch64_one<1, true, X0R>(a) : launch64_one<1, false, X0R>(a);

@@ -71,21 +71,11 @@ __device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
 // and the inputs with t' in [h*R'/2, (h+1)*R'/2), which come from the same
 // half.  Reads go to fresh SSA temporaries (compile-time renaming), so round-1
 // outputs are never overwritten by round-0 inputs.
-#ifndef RFA_TWREAD1
-#define RFA_TWREAD1 1  // pass-1/2 twiddle reads as single ds_read_b64 (A/B builds: 0 = hipcc fuses read2)
-#endif
+// pass-1/2 twiddle reads as single ds_read_b64 (hipcc would fuse ds_read2_b64: -2.8 %,
+// profiles/r03/round3_changes_ab.txt)
 template <typename T>
-__device__ __forceinline__ float2 tw_ld(const T *p) {
-    if constexpr (RFA_TWREAD1) return lds_ld2(p);
-    else return *p;
-}
+__device__ __forceinline__ float2 tw_ld(const T *p) { return lds_ld2(p); }
 
-#ifndef RFA_XBASE
-#define RFA_XBASE 0  // A/B builds: per-round LDS write base in exchange Q (bit Q): 16 K s8 -3.7 %, 8 K f32 +2.6 %, 64 K +0.2 % vs the base pre-stage build (profiles/r03/xbase_ab.txt)
-#endif
-#ifndef RFA_XBASE_PRE
-#define RFA_XBASE_PRE 1  // own LDS base for the staged second half in the pre-stage: no v_add_u32 per ds_read_u16 (64 K s8 -1.5 %, profiles/r03/xbase_ab.txt; A/B builds: 0)
-#endif
 template <int Q, int LOGM, int PT, int KR = 2>
 __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
     // KR rounds (2: the M/2 buffer; 4: an M/4 buffer, RFA_SPLIT_STAGE) -- round h
@@ -101,25 +91,12 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     const int wbase = padw((tid - wk) * W::R + wk);  // butterfly b adds R*TPF*b
     const int rbase = padw(tid);                     // butterfly b adds TPF*b
     const int my_part = tid / (G::TPF / KR);         // NB == 1 writers only
-    // NB == 1: the thread's write base inside its round's part (runtime my_part, so the
-    // compiler keeps one base and immediate offsets; folding - h*PARTP into every
-    // address cost one v_add_u32 per ds_write)
-    int wloc = wbase - my_part * PARTP;
-#if defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (W::NB == 1 && ((RFA_XBASE >> Q) & 1))
-        asm volatile("" : "+v"(wloc));  // built here, per item: not hoisted out of the item loop
-#endif
 #pragma unroll
     for (int h = 0; h < KR; h++) {
         if constexpr (W::NB == 1) {
             if (my_part == h) {
-                if constexpr ((RFA_XBASE >> Q) & 1) {
 #pragma unroll
-                    for (int t = 0; t < W::R; t++) buf[wloc + padw(t * W::P)] = v[t];
-                } else {
-#pragma unroll
-                    for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
-                }
+                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
             }
         } else {
 #pragma unroll
@@ -228,30 +205,6 @@ __device__ __forceinline__ float2 add_w16(float2 acc, float2 x) {
 // (-1..-4 % kernel time, profiles/r02g/split_stage_ab.txt; the late / direct /
 // whole-frame alternatives measured slower and were removed: split_direct_ab.txt,
 // split_whole_ab.txt).
-#ifndef PRE_DIST
-#define PRE_DIST 1
-#endif
-#ifndef RFA_CWIN
-#define RFA_CWIN 1  // N = 64 K residue 1: twiddle folded into a complex window (A/B builds: 0 = separate)
-#endif
-#ifndef RFA_CMAC2X2
-#define RFA_CMAC2X2 1  // residue-1 complex-window pre-stage as interleaved point pairs (A/B builds: 0 = one chain per point)
-#endif
-#ifndef RFA_DIF_CSO
-#define RFA_DIF_CSO 1  // large-N kernel B epilogue with compile-time store offsets (A/B builds: 0)
-#endif
-#ifndef RFA_QSTAGE
-#define RFA_QSTAGE 1  // 64 K interleaved cf32: stage the next frame's first quarter of each half (QST)
-#endif
-#ifndef RFA_QSTAGE_H
-#define RFA_QSTAGE_H 0  // A/B builds: QSTB half staging for interleaved cf32 at 8 K / 16 K too (32 K always)
-#endif
-#ifndef RFA_QSTAGE_B
-#define RFA_QSTAGE_B 1  // large-N kernel B: stage the first half of the next item's z_s (QSTB)
-#endif
-#ifndef RFA_TILE
-#define RFA_TILE 1  // ring store tiles (kRingTile) in the 32 K-point kernels (A/B builds: 0 = dword stores)
-#endif
 
 // JS != 0: the frame's two halves sit JS raw elements apart in LDS (SPLIT staging).
 // CW (N = 64 K, residue 1, 8/16-bit input): the twiddle W_N^m is folded into a complex
@@ -279,7 +232,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     // the second sample of a point (x[m + M], region A under SPLIT: a negative element
     // offset) from its own base, so every ds_read_u16 takes an immediate offset
     auto lraw_t1 = [&] {
-        if constexpr (STG && RS == 2 && RFA_XBASE_PRE) return lds_opaque(lraw + tid + (JS != 0 ? JS : M));
+        if constexpr (STG && RS == 2) return lds_opaque(lraw + tid + (JS != 0 ? JS : M));
         else return lraw_t;
     }();
     const rsrc_t w_rs = CW ? make_rsrc(cw, M * 16) : make_rsrc(window_il, M * RS * 4);
@@ -290,8 +243,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
         for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, R * (M / 32) * 8);
     }
-    // loads run DIST chunks ahead of the arithmetic (RFA_PRE_DIST experiments: 1 or 2)
-    constexpr int DIST = PRE_DIST;
+    constexpr int DIST = 1;  // loads run one chunk ahead of the arithmetic
     typename Raw<FMT>::T raw[DIST + 1][C][RS];
     float win[DIST + 1][C][CW ? 4 : RS];
     // c is a template parameter throughout: every register array index below is a
@@ -305,7 +257,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG && (QCH == 0 || c < QCH)) {  // frame (QCH: its first QCH chunks) staged in LDS
-                    if (STG && RS == 2 && RFA_XBASE_PRE && j == 1) raw[s][q][j] = lraw_t1[mo];
+                    if (STG && RS == 2 && j == 1) raw[s][q][j] = lraw_t1[mo];
                     else raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
@@ -341,7 +293,7 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     auto compute = [&]<int c>() {
         constexpr int s = c % (DIST + 1);
         if constexpr (CW) {  // y_1[m] = x[m] cw0[m] + x[m + M] cw1[m]   (NativeDsp.kt:55-58 window, DIF twiddle)
-            if constexpr (RFA_CMAC2X2 && STG && C % 2 == 0) {  // two points' chains interleaved (fft_common.h cmac2x2)
+            if constexpr (STG && C % 2 == 0) {  // two points' chains interleaved (fft_common.h cmac2x2)
 #pragma unroll
                 for (int q = 0; q < C; q += 2)
                     cmac2x2(v[c * C + q], convert_raw<FMT>(raw[s][q][0]), make_float2(win[s][q][0], win[s][q][1]),
@@ -430,10 +382,6 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 // instruction (buffer_load_dwordx4 ... lds: no VGPRs, 16 B per lane), issued
 // for the NEXT work item right after the current item's last LDS exchange, so
 // the loads fly during pass 2, the dB epilogue and the next item's start.
-// cache policy of the staging DMA (A/B builds: -DSTG_POLICY='"nt "')
-#ifndef STG_POLICY
-#define STG_POLICY ""
-#endif
 template <int BYTES, int THREADS>
 __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     static_assert(BYTES % (1024 * (THREADS / 64)) == 0, "whole 1 KiB pieces per wave");
@@ -453,7 +401,7 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
         unsigned keep;
         asm volatile(
             "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-            "buffer_load_dwordx4 %2, %3, %4 offen " STG_POLICY "lds\n\ts_mov_b32 m0, %0"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
             : "=&s"(keep)
             : "s"(base + c * 1024), "v"(lane * 16), "s"(rs), "s"(c * 1024)
             : "memory");
@@ -671,7 +619,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
                 ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, QST ? QN : JS,
-                                     RFA_CWIN && RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0, QCH>(
+                                     RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0, QCH>(
                                 v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
                           : void()), ...);
             }(std::make_integer_sequence<int, RS>{});
@@ -743,7 +691,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // kRingTile (M = 32 K, fft_kernels.h): the block's elements in this kernel's store
             // tiles -- thread 64 w + l writes its outputs t' = 4j..4j+3 (t' = (t + 16) mod 32
             // after the fft-shift) as one 16-B store at w*2048 + j*256 + l*4
-            constexpr bool TILE_OK = RFA_TILE && LOGM == 15 && PT == 32 && G::TPF == 1024 && !dif;
+            constexpr bool TILE_OK = LOGM == 15 && PT == 32 && G::TPF == 1024 && !dif;
             const bool tile = TILE_OK && (a.ring_logrs & kRingTile) != 0;
             // kernel B (dif): rows residue-major too, block s (the engine reorders them)
             const rsrc_t row_rs = make_rsrc(a.rows ? a.rows + (size_t)frame * on + (dif ? (size_t)orr * M : 0) : nullptr,
@@ -793,7 +741,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 }
             }
             auto epilogue = [&](auto nat_c, auto ring_c, auto rm_c) {
-                if constexpr (dif && RFA_DIF_CSO && (DIAG & 2) == 0) {
+                if constexpr (dif && (DIAG & 2) == 0) {
                     // large-N kernel B: every store offset is a compile-time constant (residue-major
                     // rows and ring); one s_mov_b32 next to each store instead of 32 offsets hoisted
                     // out of the item loop, spilled to VGPR lanes and read back with v_readlane + s_nop 4
@@ -871,7 +819,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
     const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
-    if (RFA_CWIN && RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
+    if (RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -907,7 +855,7 @@ int ring_logrs_for(int logn) {
     if (!wide_supported(logn) || logn <= 14) return 0;
     if (logn == 16) return 1 | kRingTile2;  // fft_w64.hip store tiles
     // 32 K-point workgroups (N = 32 K .. 128 K): residue blocks in store-tile order
-    return (logn - wide_logm(logn)) | (RFA_TILE ? kRingTile : 0);
+    return (logn - wide_logm(logn)) | kRingTile;
 }
 
 template <int LOGM, int PT, int RS, bool CO>
@@ -928,11 +876,11 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
         if constexpr (stg16) {
             if (stg && a.fmt == 2) return launch_wide_one<LOGM, PT, RS, 2, false, 0, true>(a);
         }
-        if constexpr (RFA_QSTAGE && LOGM == 15 && RS == 2 && G::SLOTS == 1) {  // cf32 64 K: quarter staging (QST)
+        if constexpr (LOGM == 15 && RS == 2 && G::SLOTS == 1) {  // cf32 64 K: quarter staging (QST)
             if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
         // cf32 32 K: half staging (QSTB); at 8 K / 16 K it spills and is slower (profiles/r03/qstage_h_ab.txt)
-        if constexpr ((RFA_QSTAGE_H || LOGM == 15) && RS == 1 && G::SLOTS == 1) {
+        if constexpr (LOGM == 15 && RS == 1 && G::SLOTS == 1) {
             if (stg && a.fmt == 3) return launch_wide_one<LOGM, PT, RS, 3, false, 0, true>(a);
         }
         switch (a.fmt) {
@@ -1028,7 +976,7 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
         if (a.dif_ss < 8 || a.dif_ss > 32) return hipErrorInvalidValue;
         if (co) return launch_wide_one<kDitLogM, 32, 1, kFmtDif, true>(a);
         // QSTB: half of the next item's z_s staged by LDS-DMA (16-byte aligned scratch)
-        if (RFA_QSTAGE_B && a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0)
+        if (a.stage && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0)
             return launch_wide_one<kDitLogM, 32, 1, kFmtDif, false, 0, true>(a);
         return launch_wide_one<kDitLogM, 32, 1, kFmtDif, false>(a);
     }

@@ -20,7 +20,7 @@ tag = sys.argv[1]
 acc = collections.defaultdict(list)
 for f in sorted(glob.glob(f"gpurun_out/pmcb_{tag}_*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "fft_" in r["Kernel_Name"]:
+        if "fft_" in r["Kernel_Name"] or "fft64_kernel" in r["Kernel_Name"]:
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
 print(tag, {k: round(sum(v) / len(v)) for k, v in sorted(acc.items())})
 PY

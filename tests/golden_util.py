@@ -48,6 +48,10 @@ DB_TOL_S16_EVERY_BIN = 0.05
 # against float64, never worse than pffft's own deviation, and 0.02 dB against pffft
 # beyond pffft's error (full_row_bound; measured 0.0107 on MI355X).
 DB_TOL_BATCH_EVERY_BIN = 0.02
+# The raw every-bin distance to the reference's pffft rows on that batch: at most
+# |librfa - float64| + |pffft - float64| <= 0.02 + pffft's own 0.038 dB (measured), bar
+# 0.06 dB; the share of bins beyond 0.01 dB is asserted separately (<= 1e-5).
+DB_TOL_RAW_PFFFT = 0.06
 
 WINDOW_IDS = {"blackman": 0, "hann": 1, "none": 2}
 
@@ -98,8 +102,19 @@ def pffft_diff(got: np.ndarray, exp: np.ndarray) -> float:
 
 # Every db_diff call appends its statistics here; tests/conftest.py prints a
 # summary at the end of the session (how many bins the floor excluded, and the
-# worst difference over ALL finite bins, not only the live ones).
+# worst difference over all RESOLVABLE finite bins, not only the live ones), each
+# worst case with the test that produced it (CURRENT_TEST, set by conftest.py).
 PARITY_LOG: list[dict] = []
+CURRENT_TEST = ""
+# fp32 resolution floor: the row unit is a MAGNITUDE dB, so a bin more than RESOLVE_DB =
+# 80 dB below its row's total (Parseval) level is under 1e-8 of it -- below what an fp32
+# FFT resolves (the reference's own pffft leaves its rounding noise 88 dB under a pure
+# tone, tests/golden kat_tone_bin_n16384_none, where the float64 transform has -126 dB).
+# A bin counts as resolvable only when BOTH sides are above that level; the others are
+# counted, never compared (db_stats' structural check still wants them deep on both
+# sides).  The session summary reports the worst difference over resolvable bins that
+# lie below the parity floor, with the test that produced it.
+RESOLVE_DB = 80.0
 
 
 def db_stats(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> dict:
@@ -118,7 +133,7 @@ def db_stats(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) ->
     assert not np.isnan(got).any(), "NaN in output"
     floor = FLOOR_DB if floor_db is None else floor_db
     worst = worst_all = 0.0
-    excluded = finite_bins = 0
+    excluded = finite_bins = subres = 0
     for g, e in zip(got, exp):
         if np.all(np.isneginf(e)):
             assert np.all(np.isneginf(g)), "expected an all -inf row (all-zero input)"
@@ -131,13 +146,15 @@ def db_stats(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) ->
         fin = np.isfinite(g) & np.isfinite(e)
         finite_bins += int(fin.sum())
         excluded += int((fin & ~live).sum())
-        if fin.any():
-            worst_all = max(worst_all, float(np.max(np.abs(g[fin] - e[fin]))))
+        res = fin & (e >= top - RESOLVE_DB) & (g >= top - RESOLVE_DB)
+        subres += int((fin & ~res).sum())
+        if res.any():
+            worst_all = max(worst_all, float(np.max(np.abs(g[res] - e[res]))))
         deep = ~live
         if deep.any():
             assert np.all(g[deep] < top - floor + 20.0), "deep bin came out shallow"
     st = {"floor_db": floor, "max_live": worst, "max_finite": worst_all, "bins": int(got.size),
-          "excluded": excluded / finite_bins if finite_bins else 0.0}
+          "excluded": excluded / finite_bins if finite_bins else 0.0, "subres": subres, "test": CURRENT_TEST}
     PARITY_LOG.append(st)
     return st
 
@@ -149,11 +166,13 @@ def db_diff(got: np.ndarray, exp: np.ndarray, floor_db: float | None = None) -> 
 
 
 FULL_ROW_LOG: list[dict] = []
+NOTES: list[str] = []  # extra lines for the session summary
 
 
-def full_row_diff(got: np.ndarray, exp: np.ndarray, bar: float | None = DB_TOL) -> float:
+def full_row_diff(got: np.ndarray, exp: np.ndarray, bar: float | None = DB_TOL, label: str = "") -> float:
     """Max |dB difference| over EVERY bin (no floor); -inf must match -inf.  ``bar`` is
-    the bar the caller asserts (logged for the session summary; None: not logged)."""
+    the bar the caller asserts (logged for the session summary; None: not logged);
+    ``label`` names the comparison in that summary."""
     got = np.atleast_2d(np.asarray(got, np.float32))
     exp = np.atleast_2d(np.asarray(exp, np.float32))
     assert got.shape == exp.shape
@@ -161,11 +180,11 @@ def full_row_diff(got: np.ndarray, exp: np.ndarray, bar: float | None = DB_TOL) 
     fin = np.isfinite(exp)
     d = float(np.max(np.abs(got[fin] - exp[fin]))) if fin.any() else 0.0
     if bar is not None:
-        FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bar": bar})
+        FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bar": bar, "label": label, "test": CURRENT_TEST})
     return d
 
 
-def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray, bar: float = DB_TOL) -> float:
+def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray, bar: float = DB_TOL, label: str = "") -> float:
     """Every bin (no floor): max over bins of |got - ref| - |ref - exact|, i.e. how far
     our row is from the reference's row beyond the reference's own distance from the
     exact (float64) transform.  Used where the reference's fp32 FFT is itself more
@@ -180,5 +199,14 @@ def full_row_bound(got: np.ndarray, ref: np.ndarray, exact: np.ndarray, bar: flo
     assert np.array_equal(np.isneginf(got), np.isneginf(ref)), "-inf bins differ"
     fin = np.isfinite(ref)
     d = float(np.max(np.abs(got[fin] - ref[fin]) - np.abs(ref[fin] - exact[fin]))) if fin.any() else 0.0
-    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bound": True, "bar": bar})
+    FULL_ROW_LOG.append({"max_full": d, "bins": int(got.size), "bound": True, "bar": bar, "label": label,
+                         "test": CURRENT_TEST})
     return d
+
+
+def exceed_fraction(got: np.ndarray, exp: np.ndarray, tol: float = DB_TOL) -> float:
+    """Share of finite bins whose |dB difference| exceeds tol."""
+    got = np.asarray(got, np.float64)
+    exp = np.asarray(exp, np.float64)
+    fin = np.isfinite(exp) & np.isfinite(got)
+    return float(np.mean(np.abs(got[fin] - exp[fin]) > tol)) if fin.any() else 0.0

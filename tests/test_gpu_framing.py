@@ -165,8 +165,10 @@ def test_legacy_calls_alternate_without_losing_the_partial_frame(rfa):
     (jni_shim.cpp handle_for): performFFT (f32, no window) between the packets of
     processIqBytesNative's framing mode (s8, Blackman) neither rebuilds that setup nor
     drops its partial frame -- every row of the reference framing arrives, and every
-    performFFT result equals the reference's pffft."""
-    n, pkt = 8192, 6000
+    performFFT result equals the reference's pffft.  (The cache is process-wide and keeps
+    a setup's partial frame by design, so this test uses a setup key -- s8, N = 2048,
+    Blackman -- that no other framing-mode test leaves half filled.)"""
+    n, pkt = 2048, 1500
     raw = signals.frames_bytes(n, 6, "s8", 11, tones=((0.21, 0.5),), noise=0.03)
     jenv = MockJNIEnv()
     fn = getattr(rfa.lib(), _P + "processIqBytesNative")
@@ -222,3 +224,24 @@ def test_legacy_unsupported_length_reports_status(rfa, m):
         good = np.zeros(2 * 64, np.float32)
         fn(jenv.env, None, jenv.new_array(np.ones(2 * 64, np.float32)), jenv.new_array(good))
         assert status() == 0
+
+
+def test_push_packet_checks_only_the_completing_packets_rate(rfa):
+    """Only the packet that completes a frame supplies the tuning
+    (Signed8BitIQConverter.java:95-97), so a partial packet with sample rate 0 is
+    accepted and buffered; a completing packet with rate 0 is an error that drops
+    the frame."""
+    n = 4096
+    raw = signals.frames_bytes(n, 3, "s8", 21, tones=((0.1, 0.5),), noise=0.02)
+    half = n  # bytes = n / 2 samples of s8 IQ
+    with rfa.SpectrumEngine(n, "blackman", "s8", ring_rows=4) as e:
+        assert e.push_packet(raw[:half], 0, 0) is False
+        assert e.pending_samples() == n // 2
+        row = e.push_packet(raw[half:2 * half], 100_000_000, 2_000_000, row=True)
+        assert row is not None
+        exp = oracle.spectrum_rows(raw[:2 * half], oracle.IN_S8, n, 1, None, oracle.WIN_BLACKMAN)[0]
+        assert gu.db_diff(row, exp) <= gu.DB_TOL
+        assert e.push_packet(raw[2 * half:3 * half], 0, 0) is False
+        with pytest.raises(Exception):
+            e.push_packet(raw[3 * half:4 * half], 100_000_000, 0)
+        assert e.pending_samples() == 0

@@ -428,6 +428,7 @@ def test_process_batches_equals_consecutive_calls(rfa, packed):
     with rfa.SpectrumEngine(n, "blackman", "s8", **kw) as a, rfa.SpectrumEngine(n, "blackman", "s8", **kw) as b:
         for e in (a, b):
             e.set_tuning(100_000_000, 2_000_000)
+            e.set_channel(99_900_000, 100_300_000)  # a squelch channel: its per-frame means
         rows_a = torch.empty((nb * fpb, n), dtype=torch.float32, device="cuda")
         a.process_batches(dev.data_ptr(), nb, stride_b, fpb, 0, rows_a.data_ptr())
         a.synchronize()
@@ -443,6 +444,10 @@ def test_process_batches_equals_consecutive_calls(rfa, packed):
         # the EMA recursion is re-associated by the chunked scan (one batch of 60 frames
         # vs five of 12): equal to fp32 rounding, not bit for bit
         np.testing.assert_allclose(a.ema(), b.ema(), rtol=0, atol=2e-4)
+        # channel means: the last batch's fpb frames in either form
+        ca, cb = a.channel_means(), b.channel_means()
+        assert ca.shape == (fpb,) and cb.shape == (fpb,)
+        np.testing.assert_array_equal(ca, cb)
 
 
 @pytest.mark.parametrize("n", [1024, 32768, 65536, 131072, 1048576])
