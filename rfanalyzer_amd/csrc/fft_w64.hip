@@ -39,9 +39,10 @@ namespace {
 
 constexpr int kM = 32768;            // points per residue item (N = 2 M)
 constexpr int kN = 65536;
-constexpr int kRow = 31;             // twiddle table row: t = 1 .. 31
-constexpr int kTw1 = 32 * kRow;      // T1[a][t - 1] = W_1024^{a t}
-constexpr int kTwLds = 2 * kTw1;     // + TB[k0][t - 1] = W_M^{t k0}
+constexpr int kRow = 31;             // TB row: t = 1 .. 31
+constexpr int kRow1 = 33;            // T1 row: t = 0 .. 31 (+1 pad: 32 rows read at once, distinct banks)
+constexpr int kTw1 = 32 * kRow1;     // T1[a][t] = W_1024^{a t}
+constexpr int kTwLds = kTw1 + 32 * kRow;  // + TB[k0][t - 1] = W_M^{t k0}
 constexpr int kPreA = kTwLds;        // blob only: W_N^c, c < 1024 (f32 residue 1)
 constexpr int kSliceA = 528;         // float2 per wave in region A: exchange-1 rounds (8 x 66) / staged half 1
 constexpr int kRegA = 16 * kSliceA;  // 8448: also the four-round exchange 0 (32 x 257 used)
@@ -51,7 +52,8 @@ constexpr int kLdsBytes = (kTwLds + kRegA + kRegB) * 8;  // 148,992 B
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
 #ifndef RFA_W64_X0R
-#define RFA_W64_X0R 4  // exchange-0 rounds: 4 through region A (half 0 staged early), 2 through A + B
+#define RFA_W64_X0R 4  // exchange 0: 4 balanced rounds through region A (default); A/B builds: 2 = writer-wave
+                       // rounds through A + B, 3 = four writer-wave rounds through A
 #endif
 
 // ---- wave-private staging: LDS-DMA of this wave's pieces x[64 w + 1024 t + half M], t < 32
@@ -131,6 +133,74 @@ __device__ __forceinline__ void exchange0(float2 (&v)[32], float2 *buf, int l, i
     }
 #pragma unroll
     for (int m = 0; m < 32; m++) v[m] = in[m / RB][m % RB];
+}
+
+// ---- exchange 0, balanced form (X0R == 4): in round h EVERY wave stores one group of 8
+// registers and loads one group of 8, so all 16 waves (4 per SIMD) write at once -- the
+// LDS store rate of ds_write_b64 needs about 4 writing waves per SIMD (MI355X_MICROARCH.md,
+// LDS), which writer-wave rounds (4 waves per round) do not have.  Round h pairs the writer
+// waves' register group g = (h - hi) & 3 (k0 bits 3-4) with the reader waves' m1 group
+// (h - hi) & 3, hi = wave bits 2-3 (= m1 bits 3-4 of a writer, k0 bits 3-4 of a reader), so a
+// round is 4 (m1-group, k0-group) pairs x 8 x 8 x 32 m0 = 64 KiB.  A reader keeps round h's
+// values in register slots 8h .. 8h+7: slot n holds m1 = (n - 8 hi) mod 32, a rotation of
+// pass 1's input by 8 hi, which multiplies its outputs by (-i)^{hi k1}.  That phase does not
+// depend on m0, so it factors out of pass 2 and |X| -- the only thing stored -- is unchanged;
+// pass 1's twiddle rows are read at the rotated index.  Element (pair p, k0lo, m1 bits 1-2,
+// m0, m1 bit 0) at p*2048 + k0lo*256 + m1b12*64 + m0*2 + m1b0, XOR 1 when k0lo is odd: a
+// store instruction covers 64 consecutive elements, a load's odd and even lanes land two
+// banks apart -- conflict-free both ways.
+__device__ __forceinline__ void exchange0_bal(float2 (&v)[32], float2 *buf, int l, int w) {
+    const int hi = w >> 2;  // wave-uniform
+    // store bases (k0lo even / odd) and load bases (m1 bit 0 even / odd)
+    // LDS byte addresses of the two store bases (the stores are inline asm)
+    unsigned wb0 = (unsigned)(size_t)(__attribute__((address_space(3))) float2 *)(buf + hi * 2048 + (w & 3) * 64 + l);
+    unsigned wb1 = (unsigned)(size_t)(__attribute__((address_space(3))) float2 *)(buf + hi * 2048 + (w & 3) * 64 + (l ^ 1));
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(wb0), "+v"(wb1));
+#endif
+    const int k0lo = ((w & 3) << 1) | (l & 1);
+    auto rd0 = lds_opaque(buf + k0lo * 256 + l);
+    auto rd1 = lds_opaque(buf + k0lo * 256 + (l ^ 1));
+    float2 in[4][8];
+#pragma unroll
+    for (int h = 0; h < 4; h++) {
+        const int g = (h - hi) & 3;  // wave-uniform: this wave's register group / reader pair this round
+        // one asm block per arm, its text tagged with the group: hipcc cannot merge the arms
+        // into one store sequence with a register select (it did, through scratch)
+        auto put = [&v, wb0, wb1](auto gc) {  // explicit: clang does not capture asm-only uses
+            constexpr int G = decltype(gc)::value;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("; exchange-0 stores, register group %18\n\t"
+                         "ds_write_b64 %0, %2\n\t"
+                         "ds_write_b64 %1, %3 offset:2048\n\t"
+                         "ds_write_b64 %0, %4 offset:4096\n\t"
+                         "ds_write_b64 %1, %5 offset:6144\n\t"
+                         "ds_write_b64 %0, %6 offset:8192\n\t"
+                         "ds_write_b64 %1, %7 offset:10240\n\t"
+                         "ds_write_b64 %0, %8 offset:12288\n\t"
+                         "ds_write_b64 %1, %9 offset:14336"
+                         :
+                         : "v"(wb0), "v"(wb1), "v"(to_v(v[8 * G])), "v"(to_v(v[8 * G + 1])), "v"(to_v(v[8 * G + 2])),
+                           "v"(to_v(v[8 * G + 3])), "v"(to_v(v[8 * G + 4])), "v"(to_v(v[8 * G + 5])),
+                           "v"(to_v(v[8 * G + 6])), "v"(to_v(v[8 * G + 7])), "i"(0), "i"(0), "i"(0), "i"(0), "i"(0),
+                           "i"(0), "i"(0), "i"(0), "i"(G)
+                         : "memory");
+#endif
+        };
+        switch (g) {  // uniform branch: the register group is a compile-time index in each arm
+        case 0: put(std::integral_constant<int, 0>{}); break;
+        case 1: put(std::integral_constant<int, 1>{}); break;
+        case 2: put(std::integral_constant<int, 2>{}); break;
+        default: put(std::integral_constant<int, 3>{}); break;
+        }
+        lds_barrier();
+        const int po = g * 2048;  // the pair this wave reads (m1 group g)
+#pragma unroll
+        for (int j = 0; j < 8; j++) in[h][j] = lds_ld2((j & 1) ? rd1 + po + (j >> 1) * 64 : rd0 + po + (j >> 1) * 64);
+        lds_barrier();
+    }
+#pragma unroll
+    for (int n = 0; n < 32; n++) v[n] = in[n >> 3][n & 7];
 }
 
 // ---- exchange 1 (wave-local): registers k1 <-> lane bits 1-5 (m0); lane bit 0 and the wave
@@ -319,19 +389,32 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
         }
         dft<32>(v);  // pass 0: m2 -> k0
         stamp(2);
-        if constexpr (STG && X0R == 4) {
+        if constexpr (STG && X0R != 2) {
             if (stage_next) stage_half(frame_ptr(fn), 0, sb, w, l);
         }
         lds_barrier();  // every wave has read its staged pieces before exchange 0 reuses region A
         stamp(3);
-        exchange0<X0R>(v, ra, l, w);
+        if constexpr (X0R == 4) exchange0_bal(v, ra, l, w);
+        else exchange0<X0R == 3 ? 4 : X0R>(v, ra, l, w);
         stamp(4);
-        // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1
+        // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1 (balanced exchange: slot n holds
+        // m1 = (n - 8 hi) mod 32, so slot group h reads its twiddles at group (h - hi) & 3)
         {
-            const float2 *row = t1 + k0 * kRow - 1;
-            v[1] = cmul(v[1], lds_ld2(row + 1));
+            const float2 *row = t1 + k0 * kRow1;
+            if constexpr (X0R == 4) {
+                const int hi = w >> 2;
 #pragma unroll
-            for (int t = 2; t < 32; t += 2) cmul2(v[t], lds_ld2(row + t), v[t + 1], lds_ld2(row + t + 1));
+                for (int h = 0; h < 4; h++) {
+                    const float2 *rg = row + ((h - hi) & 3) * 8;
+#pragma unroll
+                    for (int j = 0; j < 8; j += 2)
+                        cmul2(v[8 * h + j], lds_ld2(rg + j), v[8 * h + j + 1], lds_ld2(rg + j + 1));
+                }
+            } else {
+                v[1] = cmul(v[1], lds_ld2(row + 1));
+#pragma unroll
+                for (int t = 2; t < 32; t += 2) cmul2(v[t], lds_ld2(row + t), v[t + 1], lds_ld2(row + t + 1));
+            }
         }
         dft<32>(v);
         stamp(5);
@@ -348,7 +431,7 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
         stamp(6);
         // pass 2: twiddle W_M^{m0 (k0 + 32 k1)} = T1[k1][m0] * TB[k0][m0], DFT over m0 -> k2
         {
-            const float2 *pa_ = t1 + k1 * kRow - 1, *pb_ = tb + k0 * kRow - 1;
+            const float2 *pa_ = t1 + k1 * kRow1, *pb_ = tb + k0 * kRow - 1;
             const float2 w1 = cmul(lds_ld2(pa_ + 1), lds_ld2(pb_ + 1));
             v[1] = cmul(v[1], w1);
 #pragma unroll
@@ -449,7 +532,7 @@ hipError_t launch64_x(const FftLaunch &a) {
 
 }  // namespace
 
-// Twiddle blob (exact, correctly rounded from double): T1[a][t-1] = W_1024^{a t},
+// Twiddle blob (exact, correctly rounded from double): T1[a][t] = W_1024^{a t} (t < 33),
 // TB[k0][t-1] = W_32768^{t k0} (a, k0 < 32, t = 1..31), then W_65536^c (c < 1024).
 std::vector<float2> w64_twiddles() {
     auto w = [](double num, double den) {
@@ -458,7 +541,7 @@ std::vector<float2> w64_twiddles() {
     };
     std::vector<float2> blob;
     for (int i = 0; i < 32; i++)
-        for (int t = 1; t < 32; t++) blob.push_back(w((double)i * t, 1024.0));
+        for (int t = 0; t < kRow1; t++) blob.push_back(w((double)i * t, 1024.0));
     for (int i = 0; i < 32; i++)
         for (int t = 1; t < 32; t++) blob.push_back(w((double)t * i, (double)kM));
     for (int c = 0; c < 1024; c++) blob.push_back(w((double)c, (double)kN));
@@ -470,7 +553,10 @@ hipError_t launch_fft64(const FftLaunch &a) {
     if (a.fmt <= 2 && !a.window_cw) return hipErrorInvalidValue;
     if (a.ring && (a.ring_logrs != (1 | kRingTile2) || a.ring_rows <= 0)) return hipErrorInvalidValue;
 #ifdef RFA_AB_BUILD
-    if (const char *x = std::getenv("RFA_W64_X0R"); x && std::atoi(x) == 2) return launch64_x<2>(a);
+    if (const char *x = std::getenv("RFA_W64_X0R")) {
+        if (std::atoi(x) == 2) return launch64_x<2>(a);
+        if (std::atoi(x) == 3) return launch64_x<3>(a);
+    }
 #endif
     return launch64_x<RFA_W64_X0R>(a);
 }

@@ -50,6 +50,29 @@ def exchange0(V, rounds):
     return out
 
 
+def exchange0_bal(V):
+    """The balanced form (fft_w64.hip exchange0_bal): round h, every wave stores register
+    group (h - hi) & 3 and loads pair (h - hi) & 3 into slots 8h .. 8h+7."""
+    tid = np.arange(1024)
+    l, w = tid & 63, tid >> 6
+    hi = w >> 2
+    k0lo = ((w & 3) << 1) | (l & 1)
+    wb = [hi * 2048 + (w & 3) * 64 + l, hi * 2048 + (w & 3) * 64 + (l ^ 1)]
+    rd = [k0lo * 256 + l, k0lo * 256 + (l ^ 1)]
+    out = np.zeros_like(V)
+    for h in range(4):
+        buf = np.full(8448, np.nan, dtype=V.dtype)
+        g = (h - hi) & 3
+        for k in range(8):
+            idx = wb[k & 1] + k * 256
+            assert len(np.unique(idx)) == len(idx)
+            buf[idx] = V[tid, 8 * g + k]
+        for j in range(8):
+            out[:, 8 * h + j] = buf[rd[j & 1] + g * 2048 + (j >> 1) * 64]
+    assert not np.isnan(out).any()
+    return out
+
+
 def lane_swap32(A, B):  # one wave: A, B are [64] lane vectors (vdst, src)
     return np.concatenate([A[:32], B[:32]]), np.concatenate([A[32:], B[32:]])
 
@@ -98,8 +121,14 @@ def model_frame(x, rounds):
         m = col[:, None] + 1024 * t[None, :]
         y = (x[m] + (-1) ** r * x[m + M]) * W(m * r, N)      # pre-stage
         V = np.fft.fft(y, axis=1)                              # pass 0
-        V = exchange0(V, rounds)
-        V = V * W(k0[:, None] * t[None, :], 1024)              # W_1024^{k0 m1}
+        if rounds == "bal":
+            V = exchange0_bal(V)
+            hi = (w >> 2)[:, None]
+            m1 = (t[None, :] - 8 * hi) % 32                    # slot n holds m1 = (n - 8 hi) mod 32
+            V = V * W(k0[:, None] * m1, 1024)
+        else:
+            V = exchange0(V, rounds)
+            V = V * W(k0[:, None] * t[None, :], 1024)          # W_1024^{k0 m1}
         V = np.fft.fft(V, axis=1)                              # pass 1
         V = exchange1(V)
         V = V * W(t[None, :] * (k0 + 32 * k1)[:, None], M)     # W_M^{m0 (k0 + 32 k1)}
@@ -119,9 +148,9 @@ def test_tile2_is_a_bijection():
     assert np.array_equal(tile2_sub(p), i)
 
 
-@pytest.mark.parametrize("rounds", [4, 2])
+@pytest.mark.parametrize("rounds", [4, 2, "bal"])
 def test_w64_index_algebra_matches_fft(rounds):
-    rng = np.random.default_rng(7 + rounds)
+    rng = np.random.default_rng(7 + len(str(rounds)))
     x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
     ring, row = model_frame(x, rounds)
     ref = np.fft.fftshift(10 * np.log10(np.abs(np.fft.fft(x)) / N))
@@ -130,3 +159,37 @@ def test_w64_index_algebra_matches_fft(rounds):
     p = np.arange(N)
     nat = (tile2_sub(p & (M - 1)) << 1) | (p >> 15)
     assert np.max(np.abs(ring - ref[nat])) < 1e-9
+
+
+def _conflicts(elem_idx, kind):
+    """Extra LDS cycles of one wave instruction moving 8 B per lane (gfx950 bank model,
+    MI355X_MICROARCH.md LDS table): ds_write_b64 in 4 groups of 16 lanes, bank (a/4) mod 32;
+    ds_read_b64 in 2 groups of 32 lanes, bank (a/4) mod 64; identical addresses broadcast."""
+    size, nb = (16, 32) if kind == "w" else (32, 64)
+    extra = 0
+    for g in range(0, 64, size):
+        e = np.unique(elem_idx[g:g + size])
+        banks = np.concatenate([(2 * e) % nb, (2 * e + 1) % nb])
+        extra += np.bincount(banks, minlength=nb).max() - 1
+    return extra
+
+
+def test_w64_lds_patterns_are_conflict_free():
+    """Every LDS store / load instruction of the balanced exchange 0 and the wave-local
+    exchange 1, for every wave: no bank conflicts."""
+    l = np.arange(64)
+    for w in range(16):
+        hi = w >> 2
+        wb = [hi * 2048 + (w & 3) * 64 + l, hi * 2048 + (w & 3) * 64 + (l ^ 1)]
+        k0lo = ((w & 3) << 1) | (l & 1)
+        rd = [k0lo * 256 + l, k0lo * 256 + (l ^ 1)]
+        for k in range(8):
+            assert _conflicts(wb[k & 1] + k * 256, "w") == 0
+        for g in range(4):
+            for j in range(8):
+                assert _conflicts(rd[j & 1] + g * 2048 + (j >> 1) * 64, "r") == 0
+    rd1 = ((l >> 1) & 7) * 66 + (l & 0x31)
+    for a in range(8):
+        assert _conflicts(l + a * 66, "w") == 0
+    for b in range(8):
+        assert _conflicts(rd1 + 2 * b, "r") == 0
