@@ -105,6 +105,7 @@ struct FftLaunch {
     // passes, 32 phase stamps); always 0 in the product library
     int diag = 0;
     unsigned long long *stamps = nullptr;  // diag 32: [blocks][16][8] s_memrealtime phase stamps
+    int prio = 0;         // A/B builds (RFA_W64_PRIO): fft_w64.hip static wave priorities (s_setprio)
     int phase_ticks = 0;  // A/B builds (RFA_PHASE_NS): persistent workgroups of the second half of
                           // the grid start this many 10-ns ticks late (phase offset between the
                           // two workgroups of a CU)

@@ -138,39 +138,39 @@ __device__ __forceinline__ void exchange0(float2 (&v)[32], float2 *buf, int l, i
 // ---- exchange 0, balanced form (X0R == 4): in round h EVERY wave stores one group of 8
 // registers and loads one group of 8, so all 16 waves (4 per SIMD) write at once -- the
 // LDS store rate of ds_write_b64 needs about 4 writing waves per SIMD (MI355X_MICROARCH.md,
-// LDS), which writer-wave rounds (4 waves per round) do not have.  Round h pairs the writer
-// waves' register group g = (h - hi) & 3 (k0 bits 3-4) with the reader waves' m1 group
-// (h - hi) & 3, hi = wave bits 2-3 (= m1 bits 3-4 of a writer, k0 bits 3-4 of a reader), so a
-// round is 4 (m1-group, k0-group) pairs x 8 x 8 x 32 m0 = 64 KiB.  A reader keeps round h's
-// values in register slots 8h .. 8h+7: slot n holds m1 = (n - 8 hi) mod 32, a rotation of
-// pass 1's input by 8 hi, which multiplies its outputs by (-i)^{hi k1}.  That phase does not
-// depend on m0, so it factors out of pass 2 and |X| -- the only thing stored -- is unchanged;
-// pass 1's twiddle rows are read at the rotated index.  Element (pair p, k0lo, m1 bits 1-2,
-// m0, m1 bit 0) at p*2048 + k0lo*256 + m1b12*64 + m0*2 + m1b0, XOR 1 when k0lo is odd: a
-// store instruction covers 64 consecutive elements, a load's odd and even lanes land two
-// banks apart -- conflict-free both ways.
+// LDS), which writer-wave rounds (4 waves per round) do not have.  Round h pairs a writer's
+// register group g = (h - hi) & 3 (k0 bits 3-4) with a reader's m1 group (h - hi) & 3, hi =
+// wave bits 2-3 (= m1 bits 3-4 of a writer, k0 bits 3-4 of a reader), so a round is 4
+// (m1 group, k0 group) pairs x 8 x 8 x 32 m0 = 64 KiB.  The writer's group is wave-uniform
+// but not compile-time: each arm of a uniform branch stores its own 8 registers by inline
+// asm whose text names the group (hipcc merged plain arms into one sequence with a register
+// select, through scratch).  A reader keeps round h's values in register slots 8h .. 8h+7,
+// so slot n holds m1 = (n - 8 hi) mod 32: pass 1's input rotated by 8 hi, which multiplies
+// its outputs by (-i)^{hi k1}, a phase that factors out of pass 2 and |X|.  (Moving them back
+// into m1 order costs 64 register moves or, as four compile-time arms, spills.)
+// Element (pair p, k0lo, m1 bits 1-2, m0, m1 bit 0) at p*2048 + k0lo*256 + m1b12*64 + m0*2 +
+// m1b0, XOR 1 when k0lo is odd: a store instruction covers 64 consecutive elements, a
+// load's odd and even lanes land two banks apart (tests/test_w64_model.py).
 __device__ __forceinline__ void exchange0_bal(float2 (&v)[32], float2 *buf, int l, int w) {
     const int hi = w >> 2;  // wave-uniform
-    // store bases (k0lo even / odd) and load bases (m1 bit 0 even / odd)
-    // LDS byte addresses of the two store bases (the stores are inline asm)
+    const int k0lo = ((w & 3) << 1) | (l & 1);
+    // LDS byte addresses of the two store bases (k0lo even / odd; the stores are inline asm)
     unsigned wb0 = (unsigned)(size_t)(__attribute__((address_space(3))) float2 *)(buf + hi * 2048 + (w & 3) * 64 + l);
     unsigned wb1 = (unsigned)(size_t)(__attribute__((address_space(3))) float2 *)(buf + hi * 2048 + (w & 3) * 64 + (l ^ 1));
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(wb0), "+v"(wb1));
 #endif
-    const int k0lo = ((w & 3) << 1) | (l & 1);
-    auto rd0 = lds_opaque(buf + k0lo * 256 + l);
+    auto rd0 = lds_opaque(buf + k0lo * 256 + l);  // load bases (m1 bit 0 even / odd)
     auto rd1 = lds_opaque(buf + k0lo * 256 + (l ^ 1));
     float2 in[4][8];
 #pragma unroll
     for (int h = 0; h < 4; h++) {
-        const int g = (h - hi) & 3;  // wave-uniform: this wave's register group / reader pair this round
-        // one asm block per arm, its text tagged with the group: hipcc cannot merge the arms
-        // into one store sequence with a register select (it did, through scratch)
-        auto put = [&v, wb0, wb1](auto gc) {  // explicit: clang does not capture asm-only uses
+        const int g = (h - hi) & 3;  // wave-uniform: this round's store group / load pair
+        // explicit captures: clang does not capture variables used only as asm operands
+        auto put = [&v, wb0, wb1](auto gc) {
             constexpr int G = decltype(gc)::value;
 #if defined(__HIP_DEVICE_COMPILE__)
-            asm volatile("; exchange-0 stores, register group %18\n\t"
+            asm volatile("; exchange-0 stores, register group %10\n\t"
                          "ds_write_b64 %0, %2\n\t"
                          "ds_write_b64 %1, %3 offset:2048\n\t"
                          "ds_write_b64 %0, %4 offset:4096\n\t"
@@ -182,19 +182,18 @@ __device__ __forceinline__ void exchange0_bal(float2 (&v)[32], float2 *buf, int 
                          :
                          : "v"(wb0), "v"(wb1), "v"(to_v(v[8 * G])), "v"(to_v(v[8 * G + 1])), "v"(to_v(v[8 * G + 2])),
                            "v"(to_v(v[8 * G + 3])), "v"(to_v(v[8 * G + 4])), "v"(to_v(v[8 * G + 5])),
-                           "v"(to_v(v[8 * G + 6])), "v"(to_v(v[8 * G + 7])), "i"(0), "i"(0), "i"(0), "i"(0), "i"(0),
-                           "i"(0), "i"(0), "i"(0), "i"(G)
+                           "v"(to_v(v[8 * G + 6])), "v"(to_v(v[8 * G + 7])), "i"(G)
                          : "memory");
 #endif
         };
-        switch (g) {  // uniform branch: the register group is a compile-time index in each arm
+        switch (g) {  // uniform branch: compile-time register indices in each arm
         case 0: put(std::integral_constant<int, 0>{}); break;
         case 1: put(std::integral_constant<int, 1>{}); break;
         case 2: put(std::integral_constant<int, 2>{}); break;
         default: put(std::integral_constant<int, 3>{}); break;
         }
         lds_barrier();
-        const int po = g * 2048;  // the pair this wave reads (m1 group g)
+        const int po = g * 2048;  // the pair this wave loads (m1 group g)
 #pragma unroll
         for (int j = 0; j < 8; j++) in[h][j] = lds_ld2((j & 1) ? rd1 + po + (j >> 1) * 64 : rd0 + po + (j >> 1) * 64);
         lds_barrier();
@@ -335,6 +334,22 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
             stage_half(frame_ptr(f0), 1, sa, w, l);
         }
     }
+#ifdef RFA_AB_BUILD
+    // A/B: static wave priorities (MI355X_MICROARCH.md, two waves per SIMD item 4): 1 = the
+    // younger half (waves 8-15) at priority 1; 2 = priority w >> 2 (the youngest wave of each
+    // SIMD first); 3 = priority 3 - (w >> 2)
+    if (a.prio == 1 && w >= 8) __builtin_amdgcn_s_setprio(1);
+    if (a.prio == 2) {
+        if (w >= 12) __builtin_amdgcn_s_setprio(3);
+        else if (w >= 8) __builtin_amdgcn_s_setprio(2);
+        else if (w >= 4) __builtin_amdgcn_s_setprio(1);
+    }
+    if (a.prio == 3) {
+        if (w < 4) __builtin_amdgcn_s_setprio(3);
+        else if (w < 8) __builtin_amdgcn_s_setprio(2);
+        else if (w < 12) __builtin_amdgcn_s_setprio(1);
+    }
+#endif
     const float db_off = -kDbPerLog2 * 32.0f;  // 2 log2 N
     int pending_st = 0;  // stores issued after this wave's last staging DMA
     int it = 0;
@@ -397,8 +412,10 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
         if constexpr (X0R == 4) exchange0_bal(v, ra, l, w);
         else exchange0<X0R == 3 ? 4 : X0R>(v, ra, l, w);
         stamp(4);
-        // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1 (balanced exchange: slot n holds
-        // m1 = (n - 8 hi) mod 32, so slot group h reads its twiddles at group (h - hi) & 3)
+        // pass 1: twiddle W_1024^{k0 m1}, DFT over m1 -> k1.  After the balanced exchange slot n
+        // holds m1 = (n - 8 hi) mod 32: its twiddle is read at that index, and the DFT of the
+        // rotated slots is (-i)^{hi k1} X[k1] -- a phase independent of m0, so it factors out
+        // of pass 2 and |X| (the only thing stored) is unchanged
         {
             const float2 *row = t1 + k0 * kRow1;
             if constexpr (X0R == 4) {
@@ -553,6 +570,7 @@ hipError_t launch_fft64(const FftLaunch &a) {
     if (a.fmt <= 2 && !a.window_cw) return hipErrorInvalidValue;
     if (a.ring && (a.ring_logrs != (1 | kRingTile2) || a.ring_rows <= 0)) return hipErrorInvalidValue;
 #ifdef RFA_AB_BUILD
+    if (const char *x = std::getenv("RFA_W64_PRIO")) const_cast<FftLaunch &>(a).prio = std::atoi(x);
     if (const char *x = std::getenv("RFA_W64_X0R")) {
         if (std::atoi(x) == 2) return launch64_x<2>(a);
         if (std::atoi(x) == 3) return launch64_x<3>(a);
