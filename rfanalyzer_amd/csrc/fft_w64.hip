@@ -312,7 +312,49 @@ __device__ __forceinline__ void prestage(float2 (&v)[32], const float *window_il
 // wave into a.stamps[block][item < 4][wave][8] (engine RFA_STAMPS_FILE, scripts/stamps_w64.py):
 // 0 item start, 1 own DMA landed, 2 pass 0 done, 3 exchange-0 entry barrier passed,
 // 4 exchange 0 done, 5 pass 1 done, 6 exchange 1 (+ DMA issue) done, 7 pass 2 + epilogue done
-template <int FMT, bool STG, int X0R, int DIAG = 0>
+// Pre-stage with deep window prefetch (8-bit staged input, PREW = 1): at the start of an item the
+// 64 VGPRs of v are dead, so all 32 window pairs of residue 0 (8 B per point) are issued at once
+// into them and each point's result overwrites its own window pair; residue 1's complex window
+// (16 B per point) goes in two waves of 16 loads, the second issued into the registers the
+// first frees point by point.  One L2 round trip per item instead of one per 4-point chunk.
+template <int FMT, int R, typename P>
+__device__ __forceinline__ void prestage_deep(float2 (&v)[32], const float *window_il, const float4 *cw, int col, P l0,
+                                              P l1) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    if constexpr (R == 0) {
+        const rsrc_t w_rs = make_rsrc(window_il, kM * 8);
+        f2v wv[32];
+#pragma unroll
+        for (int t = 0; t < 32; t++)
+            wv[t] = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, col * 8, 1024 * t * 8, 0));
+#pragma unroll
+        for (int t = 0; t < 32; t++) {
+            const f2v x0 = to_v(convert_raw<FMT>(l0[64 * t])), x1 = to_v(convert_raw<FMT>(l1[64 * t]));
+            v[t] = from_v(__builtin_elementwise_fma(x1, (f2v){wv[t].y, wv[t].y}, x0 * wv[t].x));
+        }
+    } else {
+        const rsrc_t w_rs = make_rsrc(cw, kM * 16);
+        f4v cv[16];
+        auto ld = [&](int t) {
+            return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(w_rs, col * 16, 1024 * t * 16, 0));
+        };
+        auto pt = [&](int t, f4v c) {
+            return cmac2(convert_raw<FMT>(l0[64 * t]), make_float2(c.x, c.y), convert_raw<FMT>(l1[64 * t]),
+                         make_float2(c.z, c.w));
+        };
+#pragma unroll
+        for (int q = 0; q < 16; q++) cv[q] = ld(q);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            v[q] = pt(q, cv[q]);
+            cv[q] = ld(16 + q);
+        }
+#pragma unroll
+        for (int q = 0; q < 16; q++) v[16 + q] = pt(16 + q, cv[q]);
+    }
+}
+
+template <int FMT, bool STG, int X0R, int DIAG = 0, int PREW = 0>
 __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     for (int e = threadIdx.x; e < kTwLds; e += 1024) lds[e] = a.w64_tw[e];
@@ -338,13 +380,14 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
     // A/B: static wave priorities (MI355X_MICROARCH.md, two waves per SIMD item 4): 1 = the
     // younger half (waves 8-15) at priority 1; 2 = priority w >> 2 (the youngest wave of each
     // SIMD first); 3 = priority 3 - (w >> 2)
-    if (a.prio == 1 && w >= 8) __builtin_amdgcn_s_setprio(1);
-    if (a.prio == 2) {
+    const int prio = a.prio & 15;
+    if (prio == 1 && w >= 8) __builtin_amdgcn_s_setprio(1);
+    if (prio == 2) {
         if (w >= 12) __builtin_amdgcn_s_setprio(3);
         else if (w >= 8) __builtin_amdgcn_s_setprio(2);
         else if (w >= 4) __builtin_amdgcn_s_setprio(1);
     }
-    if (a.prio == 3) {
+    if (prio == 3) {
         if (w < 4) __builtin_amdgcn_s_setprio(3);
         else if (w < 8) __builtin_amdgcn_s_setprio(2);
         else if (w < 12) __builtin_amdgcn_s_setprio(1);
@@ -387,6 +430,11 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
         {
             const rsrc_t in_rs = make_rsrc(frame_ptr(active ? frame : 0), active ? (unsigned)(kN * BPS) : 0u);
             auto run = [&](auto l0, auto l1) {
+                if constexpr (PREW && STG) {
+                    if (r == 0) prestage_deep<FMT, 0>(v, a.window_il, a.window_cw, col, l0, l1);
+                    else prestage_deep<FMT, 1>(v, a.window_il, a.window_cw, col, l0, l1);
+                    return;
+                }
                 if (r == 0) {
                     prestage<FMT, 0, STG>(v, a.window_il, a.window_cw, make_float2(0.f, 0.f), in_rs, col, l0, l1);
                 } else {
@@ -505,9 +553,9 @@ __global__ void __launch_bounds__(1024, 4) fft64_kernel(FftLaunch a) {
     }
 }
 
-template <int FMT, bool STG, int X0R, int DIAG = 0>
+template <int FMT, bool STG, int X0R, int DIAG = 0, int PREW = 0>
 hipError_t launch64_one(const FftLaunch &a) {
-    auto kern = &fft64_kernel<FMT, STG, X0R, DIAG>;
+    auto kern = &fft64_kernel<FMT, STG, X0R, DIAG, PREW>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -535,6 +583,11 @@ hipError_t launch64_x(const FftLaunch &a) {
     if ((a.diag & 32) && a.stamps) {  // phase stamps (profiling only): staged s8
         if (a.fmt != 0 || !stg) return hipErrorInvalidValue;
         return launch64_one<0, true, X0R, 32>(a);
+    }
+#endif
+#ifdef RFA_AB_BUILD
+    if (a.prio >= 16 && stg && a.fmt <= 1) {  // A/B (RFA_W64_PREW=1): deep window prefetch
+        return a.fmt == 0 ? launch64_one<0, true, X0R, 0, 1>(a) : launch64_one<1, true, X0R, 0, 1>(a);
     }
 #endif
     switch (a.fmt) {
@@ -571,6 +624,7 @@ hipError_t launch_fft64(const FftLaunch &a) {
     if (a.ring && (a.ring_logrs != (1 | kRingTile2) || a.ring_rows <= 0)) return hipErrorInvalidValue;
 #ifdef RFA_AB_BUILD
     if (const char *x = std::getenv("RFA_W64_PRIO")) const_cast<FftLaunch &>(a).prio = std::atoi(x);
+    if (const char *x = std::getenv("RFA_W64_PREW"); x && std::atoi(x) == 1) const_cast<FftLaunch &>(a).prio |= 16;
     if (const char *x = std::getenv("RFA_W64_X0R")) {
         if (std::atoi(x) == 2) return launch64_x<2>(a);
         if (std::atoi(x) == 3) return launch64_x<3>(a);
