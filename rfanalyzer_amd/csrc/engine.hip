@@ -513,7 +513,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
 #endif
     // ring row order: residue-major when the main kernel splits N into residue
     // sub-FFTs (whole-line stores per workgroup), natural otherwise
-    if (h->variant != 1 || logn > 17) h->ring_logrs = rfa::ring_logrs_for(logn);
+    if (h->variant != 1 || logn > 17) h->ring_logrs = rfa::ring_logrs_for(logn, cfg->input_format);
     // two-level twiddle table W_N^s = C[s >> sh] * F[s & (2^sh - 1)], both correctly
     // rounded from double (no device sin/cos)
     h->tw_shift = (logn + 1) / 2;

@@ -117,8 +117,11 @@ hipError_t launch_fft(const FftLaunch &a);
 // The wide kernel (32 points per thread, one M-point sub-FFT per workgroup,
 // M = 8 K / 16 K / 32 K) for N = 2^13..2^17, and kernel B of the large-N pair.
 bool wide_supported(int logn);
-// ring order (ring_pos logrs) the main kernel writes for N = 2^logn
-int ring_logrs_for(int logn);
+// ring order (ring_pos logrs) the main kernel writes for N = 2^logn and input format fmt
+int ring_logrs_for(int logn, int fmt);
+// N = 64 K: input formats (bit per rfa_input_format) that take the wave-decoupled kernel
+// (fft_w64.hip); the others take the wide kernel's two-residue form (fft_wide.hip)
+bool w64_format(int fmt);
 constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
 // sub-FFT size of the wide kernel: N itself up to 16 K, else 32 K (one
 // 32 K-point workgroup per CU) with N / 32 K residues

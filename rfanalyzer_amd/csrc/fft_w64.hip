@@ -167,9 +167,13 @@ __device__ __forceinline__ void exchange0_bal(float2 (&v)[32], float2 *buf, int 
     for (int h = 0; h < 4; h++) {
         const int g = (h - hi) & 3;  // wave-uniform: this round's store group / load pair
         // explicit captures: clang does not capture variables used only as asm operands
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wunused-lambda-capture"
         auto put = [&v, wb0, wb1](auto gc) {
             constexpr int G = decltype(gc)::value;
-#if defined(__HIP_DEVICE_COMPILE__)
+#if !defined(__HIP_DEVICE_COMPILE__)
+            (void)v; (void)wb0; (void)wb1; (void)G;
+#else
             asm volatile("; exchange-0 stores, register group %10\n\t"
                          "ds_write_b64 %0, %2\n\t"
                          "ds_write_b64 %1, %3 offset:2048\n\t"
@@ -186,6 +190,7 @@ __device__ __forceinline__ void exchange0_bal(float2 (&v)[32], float2 *buf, int 
                          : "memory");
 #endif
         };
+#pragma clang diagnostic pop
         switch (g) {  // uniform branch: compile-time register indices in each arm
         case 0: put(std::integral_constant<int, 0>{}); break;
         case 1: put(std::integral_constant<int, 1>{}); break;
@@ -601,6 +606,16 @@ hipError_t launch64_x(const FftLaunch &a) {
 }
 
 }  // namespace
+
+#ifndef RFA_W64_FORMATS
+#define RFA_W64_FORMATS 0x1f  // rfa_input_format bits that take this kernel at N = 64 K (A/B builds: -D...)
+#endif
+bool w64_format(int fmt) {
+#ifdef RFA_AB_BUILD
+    if (const char *x = std::getenv("RFA_W64_FORMATS")) return fmt >= 0 && fmt < 5 && ((std::atoi(x) >> fmt) & 1);
+#endif
+    return fmt >= 0 && fmt < 5 && ((RFA_W64_FORMATS >> fmt) & 1);
+}
 
 // Twiddle blob (exact, correctly rounded from double): T1[a][t] = W_1024^{a t} (t < 33),
 // TB[k0][t-1] = W_32768^{t k0} (a, k0 < 32, t = 1..31), then W_65536^c (c < 1024).

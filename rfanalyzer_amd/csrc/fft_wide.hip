@@ -850,10 +850,10 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
     return hipGetLastError();
 }
 
-int ring_logrs_for(int logn) {
+int ring_logrs_for(int logn, int fmt) {
     if (logn > 17 && logn <= kMaxLogN) return logn - kDitLogM;  // large-N kernel B: block s of bins S q + s
     if (!wide_supported(logn) || logn <= 14) return 0;
-    if (logn == 16) return 1 | kRingTile2;  // fft_w64.hip store tiles
+    if (logn == 16 && w64_format(fmt)) return 1 | kRingTile2;  // fft_w64.hip store tiles
     // 32 K-point workgroups (N = 32 K .. 128 K): residue blocks in store-tile order
     return (logn - wide_logm(logn)) | kRingTile;
 }
@@ -984,7 +984,9 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
     case 13: return co ? wide_by_fmt<13, 32, 1, true>(a) : wide_by_fmt<13, 32, 1, false>(a);
     case 14: return co ? wide_by_fmt<14, 32, 1, true>(a) : wide_by_fmt<14, 32, 1, false>(a);
     case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
-    case 16: return co ? wide_by_fmt<15, 32, 2, true>(a) : launch_fft64(a);  // dB: wave-decoupled kernel
+    case 16:
+        if (co) return wide_by_fmt<15, 32, 2, true>(a);
+        return w64_format(a.fmt) ? launch_fft64(a) : wide_by_fmt<15, 32, 2, false>(a);
     case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
     default: return hipErrorInvalidValue;
     }

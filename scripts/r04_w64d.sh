@@ -11,6 +11,7 @@ for rnd in 1 2; do
   V+=("base_$rnd|RFA_LIB=alt/librfa_base.so" "bal_$rnd|" "x0r3_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_X0R=3" "x0r2_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_X0R=2")
   V+=("bal_p1_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_PRIO=1" "bal_p2_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_PRIO=2" "bal_p3_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_PRIO=3")
   V+=("bal_prew_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_PREW=1" "x0r3_prew_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_PREW=1 RFA_W64_X0R=3")
+  V+=("old64_$rnd|RFA_LIB=alt/librfa_ab.so RFA_W64_FORMATS=0")
 done
 bash scripts/ab_kbench.sh gpurun_out/w64_ab_$TAG.txt "--sizes 65536 --formats s8,f32 --samples 32768000 --state" "${V[@]}" || exit $?
 rm -f gpurun_out/stamps_$TAG.bin
