@@ -486,7 +486,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         const size_t mb = 128;
         h->dit_frames = (int)std::max<size_t>(1, (mb << 20) / ((size_t)n * sizeof(float2)));
     }
-    if (logn == 16) {
+    if (logn == 16 && rfa::w64_format(cfg->input_format)) {
         std::vector<float2> blob = rfa::w64_twiddles();
         if (hipMalloc(&h->d_w64_tw, blob.size() * sizeof(float2)) != hipSuccess) return bail(RFA_ERR_NOMEM);
         if (hipMemcpy(h->d_w64_tw, blob.data(), blob.size() * sizeof(float2), hipMemcpyHostToDevice) != hipSuccess)

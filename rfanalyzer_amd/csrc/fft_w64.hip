@@ -607,8 +607,16 @@ hipError_t launch64_x(const FftLaunch &a) {
 
 }  // namespace
 
+// rfa_input_format bits that take this kernel at N = 64 K.  Product builds: none -- the
+// round-4 same-call A/B (profiles/r04/w64_ab.txt) measured it 8-10 % slower than the wide
+// kernel for every format, so it is compiled into A/B builds only (all formats, or the
+// RFA_W64_FORMATS environment mask).
 #ifndef RFA_W64_FORMATS
-#define RFA_W64_FORMATS 0x1f  // rfa_input_format bits that take this kernel at N = 64 K (A/B builds: -D...)
+#ifdef RFA_AB_BUILD
+#define RFA_W64_FORMATS 0x1f
+#else
+#define RFA_W64_FORMATS 0
+#endif
 #endif
 bool w64_format(int fmt) {
 #ifdef RFA_AB_BUILD
@@ -634,6 +642,10 @@ std::vector<float2> w64_twiddles() {
 }
 
 hipError_t launch_fft64(const FftLaunch &a) {
+#if RFA_W64_FORMATS == 0 && !defined(RFA_AB_BUILD)
+    (void)a;
+    return hipErrorInvalidValue;  // not compiled into product builds (w64_format() is false)
+#else
     if (a.logn != 16 || a.complex_out || !a.w64_tw || !a.window_il) return hipErrorInvalidValue;
     if (a.fmt <= 2 && !a.window_cw) return hipErrorInvalidValue;
     if (a.ring && (a.ring_logrs != (1 | kRingTile2) || a.ring_rows <= 0)) return hipErrorInvalidValue;
@@ -646,6 +658,7 @@ hipError_t launch_fft64(const FftLaunch &a) {
     }
 #endif
     return launch64_x<RFA_W64_X0R>(a);
+#endif
 }
 
 }  // namespace rfa
