@@ -751,9 +751,22 @@ def companions(args, ranks, result):
         result["config4"] = {"workload": f"config4: batches of 256 x 8192-pt {a4.format} frames sharded over {W} "
                                          f"GPU(s), {a4.batches_per_call} batches per rfa_process_batches call",
                              "value": round(total / el / 1e6, 2), "unit": "Msamples/s", "scaling": "strong",
-                             "us_per_batch": round(el / nb * 1e6, 3), "kernel_ms": round(k4, 4), "kernel": name4,
+                             "us_per_batch": round(el / nb * 1e6, 3), "us_per_batch_amortised_over": a4.batches_per_call,
+                             "kernel_ms": round(k4, 4), "kernel": name4,
                              "per_rank_s": [round(x, 6) for x in per],
                              **_roof(a4.batches_per_call * mine * a4.fft_size * (BPS[a4.format] + 4), k4)}
+        # the same batches one rfa_process_batches call each (per-batch latency, comparable with
+        # one-batch-per-call records): launch-bound at 256 frames
+        a1 = copy.copy(a4)
+        a1.batches_per_call = 1
+        if args.dry_run:
+            el1, _ = timed(ranks, lambda k: time.sleep(0.0005 * (1 + ranks.rank)), args.c4_steps, 1)
+        else:
+            el1, _, _, _, _, _ = run_shard(a1, ranks, args.c4_steps, 1)
+        nb1 = args.c4_steps * a1.calls_per_step
+        result["config4"]["one_batch_per_call"] = {
+            "us_per_batch": round(el1 / nb1 * 1e6, 3),
+            "value": round(nb1 * a1.frames * a1.fft_size / el1 / 1e6, 2), "unit": "Msamples/s"}
         # SURVEY §8(d) config 4 names f32 and s8: the same batches on complex-float32 input
         a4.format = "f32"
         if args.dry_run:

@@ -43,8 +43,13 @@ struct WGeo {
     static constexpr int TW_P1 = 32 * P1_ROW;
     static constexpr int LO = TPF > 256 ? 32 : 16;  // pass 2: tid = hi*LO + lo
     static constexpr int P2_ROW = R2 - 1;
-    static constexpr int TW_P2A = (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
+    // 8 K: A[hi][t] = W_8192^{16 t hi} = W_512^{t hi} is row hi of the pass-1 table (same
+    // row length 15), so pass 2 reads it there: 1.9 KB less LDS per workgroup, and 4 x 39.6 KB
+    // fit a CU -- four resident workgroups (the VGPR limit) instead of three
+    static constexpr bool A_ALIAS = LOGM == 13 && R1 == 16 && R2 == 16 && LO == 16 && TPF / LO <= 32;
+    static constexpr int TW_P2A = A_ALIAS ? 0 : (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
     static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
+    static_assert(!A_ALIAS || (32 * R1 * LO == M && P1_ROW == R2 - 1), "A rows = pass-1 rows");
     static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
     static constexpr int LDS_BYTES = (TW_LDS + SLOTS * HALFP) * 8;
 };
@@ -146,9 +151,22 @@ __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *tw
 // Pass 2 (last, radix R2): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_PT^{t b}
 // (M / TPF = PT); W_M^{t tid} = A[tid/LO][t] * B[tid%LO][t] from two exact
 // tables, the b-dependent factor is a compile-time constant.
+// RFA_W8_FMA: butterfly B's factors for t = 4 and 12 are both W_8-type (W_16^{2 or 6}), so
+// their sqrt(1/2) is left to the first adds of its DFT-16 (dft16r S0)
+template <int PT, int R2, int B>
+constexpr bool p2_s0() {
+    return RFA_W8_FMA && R2 == 16 && B > 0 && ((4 * B * (64 / PT)) & 15) == 8 && ((12 * B * (64 / PT)) & 15) == 8;
+}
 template <int PT, int R2, int T, int B>
 __device__ __forceinline__ void p2_const(float2 (&v)[PT]) {
-    v[B * R2 + T] = w64<T * B * (64 / PT)>(v[B * R2 + T]);
+    constexpr int q = T * B * (64 / PT);
+    if constexpr (p2_s0<PT, R2, B>() && (T == 4 || T == 12)) v[B * R2 + T] = w16_p<q / 4>(v[B * R2 + T]);
+    else v[B * R2 + T] = w64<q>(v[B * R2 + T]);
+}
+template <int PT, int R2, int B>
+__device__ __forceinline__ void p2_dft(float2 (&v)[PT]) {
+    if constexpr (p2_s0<PT, R2, B>()) dft16r<0, true>(&v[B * R2]);
+    else dft<R2>(&v[B * R2]);
 }
 template <int PT, int R2, int T, int... Bs>
 __device__ __forceinline__ void p2_const_t(float2 (&v)[PT], std::integer_sequence<int, Bs...>) {
@@ -164,7 +182,8 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
     using G = WGeo<LOGM, PT>;
     using W = WPass<2, LOGM, PT>;
     constexpr int R2 = G::R2;
-    const float2 *ra = twp2 + (tid / G::LO) * G::P2_ROW - 1;
+    const float2 *ra = G::A_ALIAS ? twp2 - G::TW_P1 + (tid / G::LO) * G::P1_ROW - 1  // pass-1 row tid / LO
+                                  : twp2 + (tid / G::LO) * G::P2_ROW - 1;
     const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
     {
         const float2 w1 = cmul(tw_ld(ra + 1), tw_ld(rb + 1));
@@ -179,8 +198,7 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
         for (int b = 0; b < W::NB; b++) cmul2(v[b * R2 + t], w0, v[b * R2 + t + 1], w1);
     }
     if constexpr (W::NB > 1) p2_const_all<PT, R2>(v, std::make_integer_sequence<int, R2>{});
-#pragma unroll
-    for (int b = 0; b < W::NB; b++) dft<R2>(&v[b * R2]);
+    [&]<int... Bs>(std::integer_sequence<int, Bs...>) { (p2_dft<PT, R2, Bs>(v), ...); }(std::make_integer_sequence<int, W::NB>{});
 }
 
 // x * W_16^q added to acc, with the rotation / sqrt(1/2) forms folded in.
@@ -897,7 +915,7 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
 bool wide_supported(int logn) { return logn >= 13 && logn <= 17; }
 
 // Twiddle blob for the wide kernel (layout must match WGeo): pass-1 [32][R1-1],
-// pass-2 A [TPF/LO][15], B [LO][15], pre-stage pre_a [RS][M/32], pre_b [RS][32].
+// pass-2 A [TPF/LO][15] (none at 8 K: WGeo::A_ALIAS), B [LO][15], pre-stage pre_a [RS][M/32], pre_b [RS][32].
 std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
     const int m = 1 << lm, n = 1 << logn, rs = n / m;
     const int r1 = lm >= 14 ? 32 : 16, r2 = m / (32 * r1), tpf = m / pt, lo = tpf > 256 ? 32 : 16;
@@ -908,7 +926,8 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
     std::vector<float2> blob;
     for (int k = 0; k < 32; k++)
         for (int t = 1; t < r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
-    for (int hi = 0; hi < tpf / lo; hi++)
+    const bool a_alias = lm == 13 && pt == 32;  // WGeo::A_ALIAS: A is read from the pass-1 rows
+    for (int hi = 0; hi < (a_alias ? 0 : tpf / lo); hi++)
         for (int t = 1; t < r2; t++) blob.push_back(w((double)t * hi * lo, m));
     for (int l = 0; l < lo; l++)
         for (int t = 1; t < r2; t++) blob.push_back(w((double)t * l, m));
