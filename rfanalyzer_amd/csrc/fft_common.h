@@ -220,36 +220,6 @@ RFA_HD float2 w16(float2 x) {
     }
 }
 
-// c + sqrt(1/2) * a * (-i)^Q: a W_8-type factor x * W_16^q (q = 2 mod 4) is sqrt(1/2) * p with
-// p = padd<(q-2)/4, (q+2)/4>(x, x); the sqrt(1/2) is applied by the add that consumes it (one
-// v_pk_fma_f32 instead of a v_pk_mul_f32 plus a v_pk_add_f32; rounded once instead of twice).
-#ifndef RFA_W8_FMA
-#define RFA_W8_FMA 1
-#endif
-template <int Q_>
-RFA_HD float2 pfma_r2(float2 a_, float2 c_) {
-    constexpr int Q = Q_ & 3;
-#if defined(__HIP_DEVICE_COMPILE__)
-    const f2v a = to_v(a_), c = to_v(c_), k = (f2v){kR2, kR2};
-    f2v r;
-    if constexpr (Q == 0) asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
-    else if constexpr (Q == 1) asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "s"(k), "v"(c));
-    else if constexpr (Q == 2) asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(r) : "v"(a), "s"(k), "v"(c));
-    else asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "s"(k), "v"(c));
-    return from_v(r);
-#else
-    const float2 b = rot<Q>(a_);
-    return make_float2(fmaf(b.x, kR2, c_.x), fmaf(b.y, kR2, c_.y));
-#endif
-}
-// the unscaled part p of x * W_16^q, q = 2 mod 4 (x * W_16^q = sqrt(1/2) p)
-template <int q_>
-RFA_HD float2 w16_p(float2 x) {
-    constexpr int q = q_ & 15;
-    static_assert((q & 3) == 2, "W_8-type factor");
-    return padd<(q - 2) / 4, (q + 2) / 4>(x, x);
-}
-
 // In-register forward DFTs, natural order in and out.
 RFA_HD void dft2(float2 &a, float2 &b) {
     float2 t = a;
@@ -275,31 +245,6 @@ RFA_HD void dft4r(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
     x3 = padd<0, 3>(d02, d13);  // d02 + i d13
 }
 RFA_HD void dft4(float2 &x0, float2 &x1, float2 &x2, float2 &x3) { dft4r<0, 0, 0>(x0, x1, x2, x3); }
-// dft4r whose x2 (S2) or whose x1 and x3 (S13) arrive as the unscaled parts p of W_8-type
-// products (w16_p): the sqrt(1/2) is folded into the adds (pfma_r2)
-template <int P1, int P2, int P3, bool S2, bool S13>
-RFA_HD void dft4s(float2 &x0, float2 &x1, float2 &x2, float2 &x3) {
-    float2 s02, d02;
-    if constexpr (S2) {
-        s02 = pfma_r2<P2>(x2, x0);
-        d02 = pfma_r2<P2 + 2>(x2, x0);
-    } else {
-        s02 = padd<0, P2>(x0, x2);
-        d02 = padd<0, P2 + 2>(x0, x2);
-    }
-    const float2 s13 = padd<P1, P3>(x1, x3), d13 = padd<P1, P3 + 2>(x1, x3);
-    if constexpr (S13) {
-        x0 = pfma_r2<0>(s13, s02);
-        x2 = pfma_r2<2>(s13, s02);
-        x1 = pfma_r2<1>(d13, d02);
-        x3 = pfma_r2<3>(d13, d02);
-    } else {
-        x0 = cadd(s02, s13);
-        x2 = csub(s02, s13);
-        x1 = padd<0, 1>(d02, d13);
-        x3 = padd<0, 3>(d02, d13);
-    }
-}
 
 template <int R>
 RFA_HD void dft(float2 *u);
@@ -326,43 +271,26 @@ RFA_HD void dft<8>(float2 *u) {
 #pragma unroll
     for (int q = 0; q < 8; q++) u[q] = y[q];
 }
-// ROT8: input u[8] arrives pre-rotated by (-i)^ROT8 (folded into the first adds).
-// S0 (RFA_W8_FMA): u[4] and u[12] arrive as the unscaled parts of W_8-type products.
-template <int ROT8, bool S0 = false>
+// ROT8: input u[8] arrives pre-rotated by (-i)^ROT8 (folded into the first adds)
+template <int ROT8>
 RFA_HD void dft16r(float2 *u) {
     // t = 4*t1 + t2; DFT-4 over t1, twiddle W_16^{t2 q1}, DFT-4 over t2.
-#if RFA_W8_FMA
-    dft4s<0, ROT8, 0, false, S0>(u[0], u[4], u[8], u[12]);
-#else
-    static_assert(!S0, "S0 needs RFA_W8_FMA");
     dft4r<0, ROT8, 0>(u[0], u[4], u[8], u[12]);
-#endif
     dft4(u[1], u[5], u[9], u[13]);
     dft4(u[2], u[6], u[10], u[14]);
     dft4(u[3], u[7], u[11], u[15]);
     u[5] = w16<1>(u[5]);
-    u[7] = w16<3>(u[7]);
-    u[13] = w16<3>(u[13]);
-    u[15] = w16<9>(u[15]);
-#if RFA_W8_FMA
-    u[6] = w16_p<2>(u[6]);
-    u[9] = w16_p<2>(u[9]);
-    u[11] = w16_p<6>(u[11]);
-    u[14] = w16_p<6>(u[14]);
-    dft4(u[0], u[1], u[2], u[3]);
-    dft4s<0, 0, 0, true, false>(u[4], u[5], u[6], u[7]);
-    dft4s<0, 1, 0, false, true>(u[8], u[9], u[10], u[11]);  // u[10] * W_16^4 = -i u[10], folded
-    dft4s<0, 0, 0, true, false>(u[12], u[13], u[14], u[15]);
-#else
     u[6] = w16<2>(u[6]);
+    u[7] = w16<3>(u[7]);
     u[9] = w16<2>(u[9]);
     u[11] = w16<6>(u[11]);
+    u[13] = w16<3>(u[13]);
     u[14] = w16<6>(u[14]);
+    u[15] = w16<9>(u[15]);
     dft4(u[0], u[1], u[2], u[3]);
     dft4(u[4], u[5], u[6], u[7]);
     dft4r<0, 1, 0>(u[8], u[9], u[10], u[11]);  // u[10] * W_16^4 = -i u[10], folded
     dft4(u[12], u[13], u[14], u[15]);
-#endif
     // position 4*q1 + q2 holds Y[q1 + 4 q2]
     float2 y[16];
 #pragma unroll
@@ -390,20 +318,12 @@ RFA_HD void dft<32>(float2 *u) {
     // t = 16*t1 + t2 (t1 < 2): DFT-2 over t1, twiddle W_32^{t2 q1} = W_64^{2 t2 q1}, DFT-16 over t2.
 #pragma unroll
     for (int t2 = 0; t2 < 16; t2++) dft2(u[t2], u[16 + t2]);
-    u[17] = w64<2>(u[17]); u[18] = w64<4>(u[18]); u[19] = w64<6>(u[19]);
+    u[17] = w64<2>(u[17]); u[18] = w64<4>(u[18]); u[19] = w64<6>(u[19]); u[20] = w64<8>(u[20]);
     u[21] = w64<10>(u[21]); u[22] = w64<12>(u[22]); u[23] = w64<14>(u[23]);
-    u[25] = w64<18>(u[25]); u[26] = w64<20>(u[26]); u[27] = w64<22>(u[27]);
+    u[25] = w64<18>(u[25]); u[26] = w64<20>(u[26]); u[27] = w64<22>(u[27]); u[28] = w64<24>(u[28]);
     u[29] = w64<26>(u[29]); u[30] = w64<28>(u[30]); u[31] = w64<30>(u[31]);
     dft<16>(u);
-#if RFA_W8_FMA
-    u[20] = w16_p<2>(u[20]);  // W_64^8, W_64^24: sqrt(1/2) folded into dft16r's first adds
-    u[28] = w16_p<6>(u[28]);
-    dft16r<1, true>(u + 16);  // u[24] * W_64^16 = -i u[24], folded
-#else
-    u[20] = w64<8>(u[20]);
-    u[28] = w64<24>(u[28]);
     dft16r<1>(u + 16);  // u[24] * W_64^16 = -i u[24], folded
-#endif
     // position 16*q1 + q2 holds Y[q1 + 2 q2]
     float2 y[32];
 #pragma unroll
@@ -485,6 +405,16 @@ __device__ __forceinline__ float2 lds_ld2(const __attribute__((address_space(3))
     return from_v(*(const volatile __attribute__((address_space(3))) f2v *)(p));
 }
 #endif
+// one float2 as its own ds_write_b64 (volatile: not fused into ds_write2_b64, whose two 8-bit
+// offsets force a v_add_u32 per store wherever the store's offset exceeds 2 KB)
+__device__ __forceinline__ void lds_st2(float2 *p, float2 v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(volatile __attribute__((address_space(3))) f2v *)(p) = to_v(v);
+#else
+    *p = v;
+#endif
+}
+
 
 // ----------------------------------------------------------------- input conversion
 // Raw sample words as loaded (converted later, so a prefetch holds 1 VGPR per

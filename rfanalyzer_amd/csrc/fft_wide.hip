@@ -24,6 +24,7 @@
 
 #include "fft_common.h"
 #include "fft_kernels.h"
+#include "fft_w8.h"
 
 namespace rfa {
 
@@ -98,6 +99,10 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     const int my_part = tid / (G::TPF / KR);         // NB == 1 writers only
 #pragma unroll
     for (int h = 0; h < KR; h++) {
+        // the round's write base in a register of its own: the stores then carry small positive
+        // immediates (hipcc otherwise folds -h*PARTP into each store's offset, which the 16-bit
+        // unsigned ds offset cannot hold, and adds one v_add_u32 per store)
+#ifdef RFA_AB_NOXST
         if constexpr (W::NB == 1) {
             if (my_part == h) {
 #pragma unroll
@@ -111,6 +116,22 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
                     buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * PART)] = v[b * W::R + t];
             }
         }
+#else
+        int wb = wbase - h * PARTP;
+        asm volatile("" : "+v"(wb));
+        if constexpr (W::NB == 1) {
+            if (my_part == h) {
+#pragma unroll
+                for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(t * W::P), v[t]);
+            }
+        } else {
+#pragma unroll
+            for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
+#pragma unroll
+                for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(W::R * G::TPF * b + t * W::P), v[b * W::R + t]);
+            }
+        }
+#endif
         lds_barrier();
 #pragma unroll
         for (int b = 0; b < N::NB; b++) {
@@ -133,7 +154,7 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
 
 // Pass 1: k = tid & 31 is the same for every butterfly of the thread; its
 // twiddles W_{32 R}^{t k} sit contiguously at twp1[k][t-1] (exact, from double).
-template <int LOGM, int PT>
+template <int LOGM, int PT, bool W8>
 __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *twp1) {
     using W = WPass<1, LOGM, PT>;
     const float2 *row = twp1 + (tid & 31) * WGeo<LOGM, PT>::P1_ROW - 1;
@@ -145,39 +166,39 @@ __device__ __forceinline__ void pass1(float2 (&v)[PT], int tid, const float2 *tw
             cmul2(v[b * W::R + t], tw_ld(row + t), v[b * W::R + t + 1], tw_ld(row + t + 1));
     }
 #pragma unroll
-    for (int b = 0; b < W::NB; b++) dft<W::R>(&v[b * W::R]);
+    for (int b = 0; b < W::NB; b++) dftw<W::R, W8>(&v[b * W::R]);
 }
 
 // Pass 2 (last, radix R2): k = i = tid + TPF*b.  W_M^{t i} = W_M^{t tid} * W_PT^{t b}
 // (M / TPF = PT); W_M^{t tid} = A[tid/LO][t] * B[tid%LO][t] from two exact
 // tables, the b-dependent factor is a compile-time constant.
-// RFA_W8_FMA: butterfly B's factors for t = 4 and 12 are both W_8-type (W_16^{2 or 6}), so
+// W8: butterfly B's factors for t = 4 and 12 are both W_8-type (W_16^{2 or 6}), so
 // their sqrt(1/2) is left to the first adds of its DFT-16 (dft16r S0)
-template <int PT, int R2, int B>
+template <int PT, int R2, int B, bool W8>
 constexpr bool p2_s0() {
-    return RFA_W8_FMA && R2 == 16 && B > 0 && ((4 * B * (64 / PT)) & 15) == 8 && ((12 * B * (64 / PT)) & 15) == 8;
+    return W8 && R2 == 16 && B > 0 && ((4 * B * (64 / PT)) & 15) == 8 && ((12 * B * (64 / PT)) & 15) == 8;
 }
-template <int PT, int R2, int T, int B>
+template <int PT, int R2, int T, int B, bool W8>
 __device__ __forceinline__ void p2_const(float2 (&v)[PT]) {
     constexpr int q = T * B * (64 / PT);
-    if constexpr (p2_s0<PT, R2, B>() && (T == 4 || T == 12)) v[B * R2 + T] = w16_p<q / 4>(v[B * R2 + T]);
+    if constexpr (p2_s0<PT, R2, B, W8>() && (T == 4 || T == 12)) v[B * R2 + T] = w16_p<q / 4>(v[B * R2 + T]);
     else v[B * R2 + T] = w64<q>(v[B * R2 + T]);
 }
-template <int PT, int R2, int B>
+template <int PT, int R2, int B, bool W8>
 __device__ __forceinline__ void p2_dft(float2 (&v)[PT]) {
-    if constexpr (p2_s0<PT, R2, B>()) dft16r<0, true>(&v[B * R2]);
-    else dft<R2>(&v[B * R2]);
+    if constexpr (p2_s0<PT, R2, B, W8>()) dft16w<0, true>(&v[B * R2]);
+    else dftw<R2, W8>(&v[B * R2]);
 }
-template <int PT, int R2, int T, int... Bs>
+template <int PT, int R2, int T, bool W8, int... Bs>
 __device__ __forceinline__ void p2_const_t(float2 (&v)[PT], std::integer_sequence<int, Bs...>) {
-    (p2_const<PT, R2, T, Bs + 1>(v), ...);
+    (p2_const<PT, R2, T, Bs + 1, W8>(v), ...);
 }
-template <int PT, int R2, int... Ts>
+template <int PT, int R2, bool W8, int... Ts>
 __device__ __forceinline__ void p2_const_all(float2 (&v)[PT], std::integer_sequence<int, Ts...>) {
-    (p2_const_t<PT, R2, Ts>(v, std::make_integer_sequence<int, PT / R2 - 1>{}), ...);
+    (p2_const_t<PT, R2, Ts, W8>(v, std::make_integer_sequence<int, PT / R2 - 1>{}), ...);
 }
 
-template <int LOGM, int PT>
+template <int LOGM, int PT, bool W8>
 __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *twp2) {
     using G = WGeo<LOGM, PT>;
     using W = WPass<2, LOGM, PT>;
@@ -197,8 +218,8 @@ __device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *tw
 #pragma unroll
         for (int b = 0; b < W::NB; b++) cmul2(v[b * R2 + t], w0, v[b * R2 + t + 1], w1);
     }
-    if constexpr (W::NB > 1) p2_const_all<PT, R2>(v, std::make_integer_sequence<int, R2>{});
-    [&]<int... Bs>(std::integer_sequence<int, Bs...>) { (p2_dft<PT, R2, Bs>(v), ...); }(std::make_integer_sequence<int, W::NB>{});
+    if constexpr (W::NB > 1) p2_const_all<PT, R2, W8>(v, std::make_integer_sequence<int, R2>{});
+    [&]<int... Bs>(std::integer_sequence<int, Bs...>) { (p2_dft<PT, R2, Bs, W8>(v), ...); }(std::make_integer_sequence<int, W::NB>{});
 }
 
 // x * W_16^q added to acc, with the rotation / sqrt(1/2) forms folded in.
@@ -448,11 +469,14 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // descriptor below) is wave-uniform -- say so, or hipcc wraps each buffer
     // access in a readfirstlane waterfall loop.
     const int slot = __builtin_amdgcn_readfirstlane(threadIdx.x / G::TPF);
-    const int tid = threadIdx.x - slot * G::TPF;
+    const int tid0 = threadIdx.x - slot * G::TPF;
     float2 *buf = data + slot * G::HALFP;
 
     // large-N kernel B (FMT == kFmtDif): S column residues per frame, one work item each
     constexpr bool dif = FMT == kFmtDif;
+    // the DFTs' W8 form (fft_common.h pfma_r2) for the kernel's own 8/16-bit frames (not the
+    // large-N pair's scratch, not cf32: both sit near the 0.01 dB bar in one test each, §4)
+    constexpr bool W8 = !dif && FMT <= 2;
     static_assert(!dif || (RS == 1 && G::SLOTS == 1), "large-N kernel B: one 32 K residue per workgroup");
     const int work = dif ? a.n_frames * a.dif_ss : a.n_frames;
     const int items = RS == 1 ? (work + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
@@ -565,6 +589,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     int pending_st = 0;
     auto body = [&](int u, int unext) {
         stamp(u, 0);
+        // the lane index, opaque per item: the per-thread LDS bases derived from it are then
+        // built inside the item, not hoisted out of the item loop (where they spill to scratch,
+        // and each reload is followed by a vmcnt(0) that drains the staged loads)
+        int tid = tid0;
+#ifndef RFA_AB_NOTID
+        asm volatile("" : "+v"(tid));
+#endif
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
         int z;
@@ -646,7 +677,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         // ---- FFT: pass 0 (radix 32, no twiddles), exchange, pass 1, exchange, pass 2
     #pragma unroll
         for (int b = 0; b < PT / 32; b++)
-            if constexpr (!(DIAG & 4)) dft<32>(&v[b * 32]);
+            if constexpr (!(DIAG & 4)) dftw<32, W8>(&v[b * 32]);
         stamp(u, 2);
         if constexpr (STG) {
             lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
@@ -658,7 +689,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         }
         if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
         stamp(u, 3);
-        if constexpr (!(DIAG & 4)) pass1<LOGM, PT>(v, tid, tp1);
+        if constexpr (!(DIAG & 4)) pass1<LOGM, PT, W8>(v, tid, tp1);
         if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
         stamp(u, 4);
         if constexpr (STG) {
@@ -672,7 +703,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
-        if constexpr (!(DIAG & 4)) pass2<LOGM, PT>(v, tid, tp2);
+        if constexpr (!(DIAG & 4)) pass2<LOGM, PT, W8>(v, tid, tp2);
         stamp(u, 5);
         if constexpr ((DIAG & 12) != 0) {
     #pragma unroll
