@@ -47,13 +47,6 @@ struct rfa_handle {
     int dif_pipe = 6;                 // frame groups of the pipelined front kernel (8-bit input)
     int variant = 0;                  // 1: the narrow kernel (A/B builds: RFA_KERNEL=narrow)
     int stage = 1;                    // LDS-DMA staged input in the wide kernel (A/B builds: RFA_STAGE=0 off)
-    // tail-overlapped state update (process_impl, N = 64 K): the main kernel runs as the frames
-    // of its full rounds plus one partial round, and the state update of the first part runs on
-    // a second stream during the partial round, on the CUs that round leaves idle
-    int tail_state = 1;               // A/B builds: RFA_TAIL_STATE=0 off
-    int cus = 0;
-    hipStream_t side_stream = nullptr;
-    hipEvent_t ev_split = nullptr, ev_side = nullptr;
     // profiling / ablation hooks, set only by A/B builds (-DRFA_AB_BUILD, scripts/build_variant.sh);
     // the product library reads no environment and never takes these paths
     std::string stamps_file;          // RFA_STAMPS_FILE: phase stamps appended per launch
@@ -283,20 +276,7 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
     return hipSuccess;
 }
 
-// Tail-overlapped state (rfa_handle::tail_state): the frames whose 32 K residue items fill the
-// 64 K kernel's full rounds (one persistent 1024-thread workgroup per CU, fft_wide.hip
-// launch_wide_one; items of 8 consecutive frames x 2 residues), or 0 when the batch has no
-// partial last round to overlap.  Only for the state update without a channel mean.
-static int tail_split_frames(const rfa_handle *h, int n_frames) {
-    if (!h->tail_state || h->logn != 16 || h->variant == 1 || h->cus <= 0 || h->cus % 16) return 0;
-    const int items = ((n_frames + 7) / 8) * 16;
-    if (items <= h->cus || items % h->cus == 0) return 0;
-    return (items / h->cus) * h->cus / 2;  // a multiple of 8 frames
-}
-
-// split > 0: the main kernel as two launches, frames [0, split) and [split, n_frames), with
-// split_ev recorded on the handle stream between them
-int launch_main(rfa_handle *h, FftLaunch &a, int split = 0, hipEvent_t split_ev = nullptr) {
+int launch_main(rfa_handle *h, FftLaunch &a) {
     a.stream = h->stream;
     a.logn = h->logn;
     a.tw_coarse = h->d_twc;
@@ -347,19 +327,6 @@ int launch_main(rfa_handle *h, FftLaunch &a, int split = 0, hipEvent_t split_ev 
             h->d_dit_db_cap = need / 2;
         }
         e = launch_large(h, a);
-    } else if (split > 0 && split < a.n_frames) {
-        FftLaunch a1 = a, a2 = a;
-        a1.n_frames = split;
-        a2.in = a.in + (size_t)split * (size_t)a.frame_stride;
-        a2.n_frames = a.n_frames - split;
-        if (a.rows) a2.rows = a.rows + (size_t)split * (size_t)h->n;
-        if (a.ring) {  // frame split + f of the call is frame f of the second launch
-            a2.ring_base = (int)((((long long)a.ring_base - split) % a.ring_rows + a.ring_rows) % a.ring_rows);
-            a2.ring_first = std::max(0, a.ring_first - split);
-        }
-        e = rfa::launch_fft(a1);
-        if (e == hipSuccess) e = hipEventRecord(split_ev, h->stream);
-        if (e == hipSuccess) e = rfa::launch_fft(a2);
     } else {
         e = rfa::launch_fft(a);
     }
@@ -465,7 +432,6 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (rc) { delete h; return rc; }
     auto bail = [&](int code) { rfa_destroy(h); return code; };
     if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) return bail(RFA_ERR_HIP);
-    if (hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess) h->cus = 0;
     h->stream = h->own_stream;
 
     const int n = h->n;
@@ -539,7 +505,6 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_PHASE_NS")) h->phase_ticks = std::atoi(d) / 10;
     if (const char *d = std::getenv("RFA_DIF_PIPE")) h->dif_pipe = std::max(0, std::atoi(d));
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
-    if (const char *d = std::getenv("RFA_TAIL_STATE")) h->tail_state = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
         h->stamps_file = d;
         if (hipMalloc(&h->d_stamps, kStampWords * 8) != hipSuccess) return bail(RFA_ERR_NOMEM);
@@ -625,10 +590,6 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_in);
     hipFree(h->d_rows);
     if (h->h_pinned) hipHostFree(h->h_pinned);
-    if (h->side_stream) hipStreamSynchronize(h->side_stream);
-    if (h->ev_split) hipEventDestroy(h->ev_split);
-    if (h->ev_side) hipEventDestroy(h->ev_side);
-    if (h->side_stream) hipStreamDestroy(h->side_stream);
     if (h->own_stream) hipStreamDestroy(h->own_stream);
     delete h;
     return RFA_OK;
@@ -762,18 +723,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
         a.ring_logrs = h->ring_logrs;
     }
-    // tail-overlapped state: the state update of the first part waits on the side stream for
-    // the first launch only; the rest follows the second launch on the handle stream
-    int split = need_state && !need_chan ? tail_split_frames(h, (int)n_frames) : 0;
-    if (split) {
-        if (!h->side_stream && hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking) != hipSuccess)
-            return fail(h, RFA_ERR_HIP, "side stream");
-        if (!h->ev_split && hipEventCreateWithFlags(&h->ev_split, hipEventDisableTiming) != hipSuccess)
-            return fail(h, RFA_ERR_HIP, "event");
-        if (!h->ev_side && hipEventCreateWithFlags(&h->ev_side, hipEventDisableTiming) != hipSuccess)
-            return fail(h, RFA_ERR_HIP, "event");
-    }
-    int rc = launch_main(h, a, split, h->ev_split);
+    int rc = launch_main(h, a);
     if (rc) return rc;
     if (need_state || need_chan) {
         rfa::StateLaunch s;
@@ -795,23 +745,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             s.rows = state_rows;
             s.row_stride = n;
         }
-        if (need_state && split) {
-            rfa::StateLaunch s1 = s, s2 = s;
-            s1.n_frames = split;
-            s1.stream = h->side_stream;
-            s2.n_frames = (int)n_frames - split;
-            if (rows_in_ring)
-                s2.ring_base = (int)((((long long)h->write_index - split) % h->ring_rows + h->ring_rows) % h->ring_rows);
-            else
-                s2.rows = state_rows + (size_t)split * n;
-            HIPCHK(h, hipStreamWaitEvent(h->side_stream, h->ev_split, 0));
-            HIPCHK(h, rfa::launch_state(s1));
-            HIPCHK(h, hipEventRecord(h->ev_side, h->side_stream));
-            HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_side, 0));
-            HIPCHK(h, rfa::launch_state(s2));
-        } else if (need_state) {
-            HIPCHK(h, rfa::launch_state(s));
-        }
+        if (need_state) HIPCHK(h, rfa::launch_state(s));
         if (need_chan) {
             // means, then (channels wider than 16384 bins) the per-span partial sums
             const int spans = rfa::channel_mean_spans(chan_last - chan_first);

@@ -82,7 +82,7 @@ __device__ __forceinline__ constexpr int padw(int e) { return e + (e >> 5); }
 template <typename T>
 __device__ __forceinline__ float2 tw_ld(const T *p) { return lds_ld2(p); }
 
-template <int Q, int LOGM, int PT, int KR = 2>
+template <int Q, int LOGM, int PT, int KR = 2, bool XST = false>
 __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) {
     // KR rounds (2: the M/2 buffer; 4: an M/4 buffer, RFA_SPLIT_STAGE) -- round h
     // moves the outputs landing in [h*M/KR, (h+1)*M/KR) and the inputs t' in
@@ -99,39 +99,42 @@ __device__ __forceinline__ void exchange(float2 (&v)[PT], float2 *buf, int tid) 
     const int my_part = tid / (G::TPF / KR);         // NB == 1 writers only
 #pragma unroll
     for (int h = 0; h < KR; h++) {
-        // the round's write base in a register of its own: the stores then carry small positive
-        // immediates (hipcc otherwise folds -h*PARTP into each store's offset, which the 16-bit
-        // unsigned ds offset cannot hold, and adds one v_add_u32 per store)
-#ifdef RFA_AB_NOXST
-        if constexpr (W::NB == 1) {
-            if (my_part == h) {
+        // XST (staged persistent kernels): the round's write base in a register of its own and
+        // one ds_write_b64 per output, so every store carries a small positive immediate (hipcc
+        // otherwise folds -h*PARTP into each store's offset, which the unsigned ds offset cannot
+        // hold, or fuses pairs into ds_write2_b64, whose 8-bit offsets cannot either, and adds a
+        // v_add_u32 per store): -2 .. -3 % at 8 K / 16 K s8 (profiles/r04/vadd2_ab.txt); the
+        // one-item-per-workgroup cf32 8 K kernel is 5 % slower with it, so it keeps the plain form
+        if constexpr (!XST) {
+            if constexpr (W::NB == 1) {
+                if (my_part == h) {
 #pragma unroll
-                for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
+                    for (int t = 0; t < W::R; t++) buf[wbase + padw(t * W::P) - h * PARTP] = v[t];
+                }
+            } else {
+#pragma unroll
+                for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
+#pragma unroll
+                    for (int t = 0; t < W::R; t++)
+                        buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * PART)] = v[b * W::R + t];
+                }
             }
         } else {
+            int wb = wbase - h * PARTP;
+            asm volatile("" : "+v"(wb));
+            if constexpr (W::NB == 1) {
+                if (my_part == h) {
 #pragma unroll
-            for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
+                    for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(t * W::P), v[t]);
+                }
+            } else {
 #pragma unroll
-                for (int t = 0; t < W::R; t++)
-                    buf[wbase + padw(W::R * G::TPF * b + t * W::P - h * PART)] = v[b * W::R + t];
+                for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
+#pragma unroll
+                    for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(W::R * G::TPF * b + t * W::P), v[b * W::R + t]);
+                }
             }
         }
-#else
-        int wb = wbase - h * PARTP;
-        asm volatile("" : "+v"(wb));
-        if constexpr (W::NB == 1) {
-            if (my_part == h) {
-#pragma unroll
-                for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(t * W::P), v[t]);
-            }
-        } else {
-#pragma unroll
-            for (int b = h * W::NB / KR; b < (h + 1) * W::NB / KR; b++) {
-#pragma unroll
-                for (int t = 0; t < W::R; t++) lds_st2(buf + wb + padw(W::R * G::TPF * b + t * W::P), v[b * W::R + t]);
-            }
-        }
-#endif
         lds_barrier();
 #pragma unroll
         for (int b = 0; b < N::NB; b++) {
@@ -593,9 +596,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         // built inside the item, not hoisted out of the item loop (where they spill to scratch,
         // and each reload is followed by a vmcnt(0) that drains the staged loads)
         int tid = tid0;
-#ifndef RFA_AB_NOTID
         asm volatile("" : "+v"(tid));
-#endif
         // opaque zero: stops hipcc hoisting the (loop-invariant) twiddle-table
         // reads out of the item loop, which would need ~90 more VGPRs
         int z;
@@ -687,10 +688,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 if (unext < items && fn < a.n_frames) stage_half(fn, 0);
             }
         }
-        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR>(v, buf, tid);
+        if constexpr (!(DIAG & 8)) exchange<0, LOGM, PT, KR, STG>(v, buf, tid);
         stamp(u, 3);
         if constexpr (!(DIAG & 4)) pass1<LOGM, PT, W8>(v, tid, tp1);
-        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR>(v, buf, tid);
+        if constexpr (!(DIAG & 8)) exchange<1, LOGM, PT, KR, STG>(v, buf, tid);
         stamp(u, 4);
         if constexpr (STG) {
             // exchange 1 ended with a barrier after its last reads: the buffer is free
