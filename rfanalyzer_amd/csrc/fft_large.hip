@@ -124,26 +124,32 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
 // no VGPRs) right after every wave has read the current one, so it lands while
 // this frame is transformed and its z stores drain: loads and stores of a block
 // overlap instead of every block loading, then storing, in lock step.
-template <int S, int FMT>
-__global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int groups) {
+#ifndef RFA_DIF_BW
+#define RFA_DIF_BW 256
+#endif
+// BW columns per block (RFA_DIF_BW, A/B): the D table is one LDS copy per block, so 512-column
+// blocks hold half the table bytes per wave of 256-column ones
+template <int S, int FMT, int BW = RFA_DIF_BW>
+__global__ void __launch_bounds__(BW, BW >= 512 ? 2 : 1) dif_front_pipe_kernel(DifLaunch a, int groups) {
     static_assert(FMT <= 1, "8-bit formats");
     constexpr int M = 1 << kDitLogM, n = S * M, mc = M >> 7;
-    constexpr int SB = 2;
-    constexpr int ROWB = 256 * SB, TILEB = S * ROWB, NPIECE = TILEB / 1024, PPW = NPIECE / 4;
-    constexpr int RPP = 1024 / ROWB, LPR = 64 / RPP;  // tile rows per 1 KiB piece, lanes per row
-    static_assert(NPIECE % 4 == 0 && RPP >= 1, "whole pieces per wave");
+    constexpr int SB = 2, NW = BW / 64;
+    constexpr int ROWB = BW * SB, TILEB = S * ROWB, NPIECE = TILEB / 1024, PPW = NPIECE / NW;
+    constexpr int RPP = ROWB >= 1024 ? 1 : 1024 / ROWB, LPR = 64 / RPP;  // tile rows per 1 KiB piece, lanes per row
+    constexpr int PPR = ROWB >= 1024 ? ROWB / 1024 : 1;                   // 1 KiB pieces per tile row
+    static_assert(NPIECE % NW == 0 && RPP >= 1, "whole pieces per wave");
     __shared__ __attribute__((aligned(16))) uint8_t tile[TILEB];
     __shared__ float2 dtab[S * 128];
-    const int bx = blockIdx.x % (M / 256), g0 = blockIdx.x / (M / 256);
-    const int m0 = bx * 256, m = m0 + threadIdx.x;
+    const int bx = blockIdx.x % (M / BW), g0 = blockIdx.x / (M / BW);
+    const int m0 = bx * BW, m = m0 + threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const unsigned tbase = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)tile;
     auto stage = [&](int f) {  // this wave's PPW pieces of frame f's tile (inline asm: see stage_frame)
         const rsrc_t rs = make_rsrc(a.in + (size_t)f * (size_t)a.frame_stride, n * SB);
 #pragma unroll
         for (int i = 0; i < PPW; i++) {
-            const int pc = wave * PPW + i, j = pc * RPP + lane / LPR;
-            const int voff = (j * M + m0) * SB + (lane % LPR) * 16;
+            const int pc = wave * PPW + i, j = (pc / PPR) * RPP + lane / LPR;
+            const int voff = (j * M + m0) * SB + (pc % PPR) * 1024 + (lane % LPR) * 16;
             unsigned keep;
             asm volatile(
                 "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
@@ -153,7 +159,7 @@ __global__ void __launch_bounds__(256) dif_front_pipe_kernel(DifLaunch a, int gr
                 : "memory");
         }
     };
-    for (int e = threadIdx.x; e < S * 128; e += 256) dtab[e] = a.tw_d[e];
+    for (int e = threadIdx.x; e < S * 128; e += BW) dtab[e] = a.tw_d[e];
     const rsrc_t w_rs = make_rsrc(a.window, n * 4);
     float w[S];
 #pragma unroll
@@ -202,10 +208,10 @@ static hipError_t launch_s(const DifLaunch &a) {
     const dim3 grid((1 << kDitLogM) / 256, a.n_frames);
     // pipelined kernel: 8-bit input (16-bit measured slower: its 64 KB of LDS halves the resident blocks)
     if (a.pipe > 0 && a.fmt <= 1 && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0) {
-        const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = 128 x groups
-        const dim3 pg((1 << kDitLogM) / 256 * groups);
-        if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(256), 0, a.stream, a, groups);
-        else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(256), 0, a.stream, a, groups);
+        const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = (M / BW) x groups
+        const dim3 pg((1 << kDitLogM) / RFA_DIF_BW * groups);
+        if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(RFA_DIF_BW), 0, a.stream, a, groups);
+        else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(RFA_DIF_BW), 0, a.stream, a, groups);
         return hipGetLastError();
     }
     switch (a.fmt) {
