@@ -124,12 +124,9 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
 // no VGPRs) right after every wave has read the current one, so it lands while
 // this frame is transformed and its z stores drain: loads and stores of a block
 // overlap instead of every block loading, then storing, in lock step.
-#ifndef RFA_DIF_BW
-#define RFA_DIF_BW 256
-#endif
-// BW columns per block (RFA_DIF_BW, A/B): the D table is one LDS copy per block, so 512-column
-// blocks hold half the table bytes per wave of 256-column ones
-template <int S, int FMT, int BW = RFA_DIF_BW>
+// BW columns per block.  512-column blocks (one D table per 8 waves, 4 waves per SIMD) measured
+// -1.4 % at 1 M with the ring and +3 % at 256 K / 512 K (profiles/r04/dif_block_width_ab.txt)
+template <int S, int FMT, int BW = 256>
 __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : 1) dif_front_pipe_kernel(DifLaunch a, int groups) {
     static_assert(FMT <= 1, "8-bit formats");
     constexpr int M = 1 << kDitLogM, n = S * M, mc = M >> 7;
@@ -209,9 +206,9 @@ static hipError_t launch_s(const DifLaunch &a) {
     // pipelined kernel: 8-bit input (16-bit measured slower: its 64 KB of LDS halves the resident blocks)
     if (a.pipe > 0 && a.fmt <= 1 && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0) {
         const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = (M / BW) x groups
-        const dim3 pg((1 << kDitLogM) / RFA_DIF_BW * groups);
-        if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(RFA_DIF_BW), 0, a.stream, a, groups);
-        else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(RFA_DIF_BW), 0, a.stream, a, groups);
+        const dim3 pg((1 << kDitLogM) / 256 * groups);
+        if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(256), 0, a.stream, a, groups);
+        else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(256), 0, a.stream, a, groups);
         return hipGetLastError();
     }
     switch (a.fmt) {

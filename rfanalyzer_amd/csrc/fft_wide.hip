@@ -28,9 +28,6 @@
 
 namespace rfa {
 
-#ifndef RFA_P2DIRECT
-#define RFA_P2DIRECT 0
-#endif
 template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
@@ -51,12 +48,8 @@ struct WGeo {
     // row length 15), so pass 2 reads it there: 1.9 KB less LDS per workgroup, and 4 x 39.6 KB
     // fit a CU -- four resident workgroups (the VGPR limit) instead of three
     static constexpr bool A_ALIAS = LOGM == 13 && R1 == 16 && R2 == 16 && LO == 16 && TPF / LO <= 32;
-    // P2D (8 K / 16 K): pass 2 reads its twiddles W_M^{t i} (i = tid + TPF b, the butterfly's
-    // full index) from a direct table in global memory (L2-resident, 64 / 128 KB): no A x B
-    // products, no W_PT^{t b} constants, no LDS rows for A and B
-    static constexpr bool P2D = RFA_P2DIRECT && (LOGM == 13 || LOGM == 14) && R2 == 16;
-    static constexpr int TW_P2A = (A_ALIAS || P2D) ? 0 : (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
-    static constexpr int TW_P2B = P2D ? 0 : LO * P2_ROW;  // B[lo][t] = W_M^{t lo}
+    static constexpr int TW_P2A = A_ALIAS ? 0 : (TPF / LO) * P2_ROW;  // A[hi][t] = W_M^{t hi LO}
+    static constexpr int TW_P2B = LO * P2_ROW;          // B[lo][t] = W_M^{t lo}
     static_assert(!A_ALIAS || (32 * R1 * LO == M && P1_ROW == R2 - 1), "A rows = pass-1 rows");
     static constexpr int TW_LDS = TW_P1 + TW_P2A + TW_P2B;
     static constexpr int LDS_BYTES = (TW_LDS + SLOTS * HALFP) * 8;
@@ -209,33 +202,10 @@ __device__ __forceinline__ void p2_const_all(float2 (&v)[PT], std::integer_seque
 }
 
 template <int LOGM, int PT, bool W8>
-__device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *twp2, const float2 *wide_tw) {
+__device__ __forceinline__ void pass2(float2 (&v)[PT], int tid, const float2 *twp2) {
     using G = WGeo<LOGM, PT>;
     using W = WPass<2, LOGM, PT>;
     constexpr int R2 = G::R2;
-    if constexpr (G::P2D) {
-        // direct rows D[i][t] = W_M^{t i}, t = 0 .. 15 (128 B per i, t = 0 unused): per butterfly
-        // 8 x 16-B loads of the pairs (t, t + 1)
-        const rsrc_t d_rs = make_rsrc(wide_tw + G::TW_LDS, (unsigned)(G::M / R2) * R2 * 8);
-        typedef float f4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-        for (int b = 0; b < W::NB; b++) {
-            f4v w[R2 / 2];
-#pragma unroll
-            for (int t2 = 0; t2 < R2 / 2; t2++)
-                w[t2] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(d_rs, (tid + G::TPF * b) * (R2 * 8),
-                                                                                      t2 * 16, 0));
-            v[b * R2 + 1] = cmul(v[b * R2 + 1], make_float2(w[0].z, w[0].w));
-#pragma unroll
-            for (int t = 2; t < R2; t += 2)
-                cmul2(v[b * R2 + t], make_float2(w[t / 2].x, w[t / 2].y), v[b * R2 + t + 1],
-                      make_float2(w[t / 2].z, w[t / 2].w));
-            __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-        for (int b = 0; b < W::NB; b++) dftw<R2, W8>(&v[b * R2]);
-        return;
-    }
     const float2 *ra = G::A_ALIAS ? twp2 - G::TW_P1 + (tid / G::LO) * G::P1_ROW - 1  // pass-1 row tid / LO
                                   : twp2 + (tid / G::LO) * G::P2_ROW - 1;
     const float2 *rb = twp2 + G::TW_P2A + (tid % G::LO) * G::P2_ROW - 1;
@@ -734,7 +704,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 else stage_frame<M * RS * BPS, G::THREADS>(a.in + (size_t)fn * (size_t)a.frame_stride, buf);
             }
         }
-        if constexpr (!(DIAG & 4)) pass2<LOGM, PT, W8>(v, tid, tp2, a.wide_tw);
+        if constexpr (!(DIAG & 4)) pass2<LOGM, PT, W8>(v, tid, tp2);
         stamp(u, 5);
         if constexpr ((DIAG & 12) != 0) {
     #pragma unroll
@@ -988,16 +958,11 @@ std::vector<float2> wide_twiddles(int logn, int pt, int lm) {
     std::vector<float2> blob;
     for (int k = 0; k < 32; k++)
         for (int t = 1; t < r1; t++) blob.push_back(w((double)t * k, 32.0 * r1));
-    const bool p2d = RFA_P2DIRECT && (lm == 13 || lm == 14) && r2 == 16 && pt == 32;  // WGeo::P2D
     const bool a_alias = lm == 13 && pt == 32;  // WGeo::A_ALIAS: A is read from the pass-1 rows
-    for (int hi = 0; hi < ((a_alias || p2d) ? 0 : tpf / lo); hi++)
+    for (int hi = 0; hi < (a_alias ? 0 : tpf / lo); hi++)
         for (int t = 1; t < r2; t++) blob.push_back(w((double)t * hi * lo, m));
-    for (int l = 0; l < (p2d ? 0 : lo); l++)
+    for (int l = 0; l < lo; l++)
         for (int t = 1; t < r2; t++) blob.push_back(w((double)t * l, m));
-    if (p2d) {  // pass-2 direct rows D[i][t] = W_M^{t i}, i < M / 16, t < 16 (after the LDS part; rs == 1)
-        for (int i = 0; i < m / r2; i++)
-            for (int t = 0; t < r2; t++) blob.push_back(w((double)t * i, m));
-    }
     if (rs > 1) {
         for (int r = 0; r < rs; r++)
             for (int mp = 0; mp < m / 32; mp++) blob.push_back(w((double)mp * r, n));
