@@ -28,9 +28,6 @@
 
 namespace rfa {
 
-#ifndef RFA_PRE_DIST_F32
-#define RFA_PRE_DIST_F32 1
-#endif
 template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
@@ -288,8 +285,9 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
 #pragma unroll
         for (int b = 0; b < PT / 32; b++) pa[b] = buf_load_f32x2(pa_rs, (tid + G::TPF * b) * 8, R * (M / 32) * 8);
     }
-    // loads run DIST chunks ahead of the arithmetic (RFA_PRE_DIST_F32, A/B: 64 K float input)
-    constexpr int DIST = (FMT >= 3 && RS == 2) ? RFA_PRE_DIST_F32 : 1;
+    // loads run one chunk ahead of the arithmetic (two for 64 K float input: ±1 %,
+    // profiles/r04/prestage_distance_f32_ab.txt)
+    constexpr int DIST = 1;
     typename Raw<FMT>::T raw[DIST + 1][C][RS];
     float win[DIST + 1][C][CW ? 4 : RS];
     // c is a template parameter throughout: every register array index below is a
