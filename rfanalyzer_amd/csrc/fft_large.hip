@@ -205,7 +205,7 @@ static hipError_t launch_s(const DifLaunch &a) {
     const dim3 grid((1 << kDitLogM) / 256, a.n_frames);
     // pipelined kernel: 8-bit input (16-bit measured slower: its 64 KB of LDS halves the resident blocks)
     if (a.pipe > 0 && a.fmt <= 1 && ((reinterpret_cast<uintptr_t>(a.in) | (uintptr_t)a.frame_stride) & 15) == 0) {
-        const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = (M / BW) x groups
+        const int groups = std::min(a.n_frames, a.pipe);  // frame groups: blocks = (M / 256) x groups
         const dim3 pg((1 << kDitLogM) / 256 * groups);
         if (a.fmt == 0) hipLaunchKernelGGL((dif_front_pipe_kernel<S, 0>), pg, dim3(256), 0, a.stream, a, groups);
         else hipLaunchKernelGGL((dif_front_pipe_kernel<S, 1>), pg, dim3(256), 0, a.stream, a, groups);
