@@ -1,4 +1,5 @@
-// gfx950 64 K-point kernel, wave-decoupled form.
+// gfx950 64 K-point kernel, wave-decoupled form: A/B builds only (DESIGN.md §6.3 -- measured 8-10 %
+// slower than the wide kernel, profiles/r04/w64_ab.txt; product builds keep fft_wide.hip for N = 64 K).
 //
 // Same per-frame pipeline as the wide kernel (fft_wide.hip): raw IQ -> LUT-exact convert ->
 // window (fp32 multiply, NativeDsp.kt:55-58) -> radix-2 decimation-in-frequency pre-stage
