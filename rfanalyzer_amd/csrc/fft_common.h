@@ -551,9 +551,15 @@ __device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float
     i32x4 v = {__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), __builtin_bit_cast(int, c),
                __builtin_bit_cast(int, d)};
 #if defined(__HIP_DEVICE_COMPILE__)
+#if defined(RFA_ST_SC1)  // A/B: write-through stores that drop the line from the XCD L2
+    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
+                 "s"(soff)
+                 : "memory");
+#else
     asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
                  "s"(soff)
                  : "memory");
+#endif
 #else
     (void)v; (void)rs; (void)voff; (void)soff;
 #endif
