@@ -551,15 +551,13 @@ __device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float
     i32x4 v = {__builtin_bit_cast(int, a), __builtin_bit_cast(int, b), __builtin_bit_cast(int, c),
                __builtin_bit_cast(int, d)};
 #if defined(__HIP_DEVICE_COMPILE__)
-#if defined(RFA_ST_SC1)  // A/B: write-through stores that drop the line from the XCD L2
+    // sc1: write-through, the line leaves the XCD's L2 (MI355X_MICROARCH.md, store flavours), so
+    // the ring's 128 KB per 32 K item no longer evicts the window tables and the staged frames:
+    // FETCH 91.0 -> 81.7 MB per 64 K launch, 64 K cf32 -2.4 %, 128 K -3 .. -6 %, 64 K s8 +-0
+    // (profiles/r04/ring_store_sc1_ab.txt)
     asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen sc1\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
                  "s"(soff)
                  : "memory");
-#else
-    asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 1" ::"v"(v), "v"(voff), "s"(rs),
-                 "s"(soff)
-                 : "memory");
-#endif
 #else
     (void)v; (void)rs; (void)voff; (void)soff;
 #endif
