@@ -118,3 +118,14 @@ def test_product_library_reads_no_environment(lib):
     r = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert "getenv" not in r.stdout
+
+
+def test_product_library_ships_only_the_wide_64k_kernel(lib):
+    """N = 64 K runs the wide kernel in product builds: the wave-decoupled kernel
+    (fft_w64.hip, measured 8-10 % slower, profiles/r04/w64_ab.txt) is compiled into A/B
+    builds only, so its code object is absent from the product librfa.so."""
+    from rfanalyzer_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as fh:
+        blob = fh.read()
+    assert b"fft64_kernel" not in blob
+    assert b"fft_wide_kernel" in blob
