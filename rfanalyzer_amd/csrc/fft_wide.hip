@@ -28,9 +28,6 @@
 
 namespace rfa {
 
-#ifndef RFA_RES_ROTATE
-#define RFA_RES_ROTATE 0
-#endif
 template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
@@ -617,15 +614,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                 dif_r = u - frame * a.dif_ss;
             }
         } else {
-            // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only)
+            // blocks b, b+8, b+16, ... share an XCD: put a frame's RS residues there (speed only).
+            // A workgroup keeps one residue across its items (rotating it by the round: +0.3 ..
+            // +1.2 %, profiles/r04/residue_rotation_ab.txt)
             const int g = u / (8 * RS), rem = u - g * (8 * RS);
             r = rem >> 3;
-#if RFA_RES_ROTATE
-            // RFA_RES_ROTATE (A/B): rotate the residue by the round, so a persistent workgroup
-            // alternates the residues' pre-stages (residue 1's is the heavier) instead of always
-            // running the same one; a frame's RS items stay in one round (grid multiple of 8 RS)
-            if ((int)gridDim.x % (8 * RS) == 0) r = (r + u / (int)gridDim.x) % RS;
-#endif
             frame = g * 8 + (rem & 7);
         }
         const bool active = frame < a.n_frames;
