@@ -297,6 +297,25 @@ RFA_API int rfa_fft_logmag_interleaved(rfa_handle *h, const float *in, float *ma
 /* nativedsp.cpp:19-42: ordered, unscaled, forward complex FFT, 2N floats each. */
 RFA_API int rfa_fft_ordered(rfa_handle *h, const float *in, float *out, size_t n);
 
+/* The same three seams at every length the reference's pffft accepts
+ * (pffft_new_setup, pffft.c:1231-1280: N a multiple of 16, N / 4 a product of
+ * 2, 3, 4 and 5, N <= 2^26), one plan per N like nativedsp.cpp:12-17's cached
+ * setup.  rfa_create covers the powers of two 64 .. 2^20 with its fused kernels;
+ * a plan serves the rest (16, 32, 2^21 .. 2^26, mixed lengths such as 48 or
+ * 3 * 2^20) with a mixed-radix Stockham FFT on the GPU (csrc/fft_seam.hip).
+ * rfa_seam_create returns RFA_ERR_UNSUPPORTED for a length pffft rejects.
+ * Synchronous, host arrays, RFA_ERR_SIZE on a length mismatch. */
+typedef struct rfa_seam rfa_seam;
+RFA_API int rfa_seam_supported(int32_t n); /* 1 when pffft accepts N, else 0 */
+RFA_API int rfa_seam_create(int32_t n, int32_t device_id, rfa_seam **out);
+RFA_API int rfa_seam_destroy(rfa_seam *s);
+RFA_API const char *rfa_seam_last_error(const rfa_seam *s);
+/* the pass radices (8, 4, 2, 3, 5), first pass first; count = number of passes */
+RFA_API int rfa_seam_get_plan(const rfa_seam *s, int32_t *radices, int32_t cap, int32_t *count);
+RFA_API int rfa_seam_windowed_fft_mag_planar(rfa_seam *s, const float *re, const float *im, float *mag_out, size_t n);
+RFA_API int rfa_seam_fft_logmag_interleaved(rfa_seam *s, const float *in, float *mag_out, size_t n);
+RFA_API int rfa_seam_fft_ordered(rfa_seam *s, const float *in, float *out, size_t n);
+
 /* Profiling: while enabled, HIP events bracket every main FFT kernel launch on
  * the handle stream; rfa_get_kernel_time waits for and sums them.  Toggling
  * never synchronises, so a caller may profile a sample of its launches. */

@@ -57,9 +57,11 @@ JNIEXPORT int rfa_jni_abi_version(void);
 /* Status of the last legacy call (performFFT, performFFTAndLogMag,
  * performWindowedFftAndReturnMagNative, processIqBytesNative), whose JNI signatures
  * return nothing (nativedsp.cpp:19-81): RFA_OK, or e.g. RFA_ERR_UNSUPPORTED when the
- * length is one the reference's pffft accepts (N = 2^a 3^b 5^c, a multiple of 16,
- * pffft.c:1236-1247) but librfa does not (N a power of two, 64 .. 2^20) -- the output
- * array is then left untouched. */
+ * reference's pffft rejects the length too (not a multiple of 16, a factor other than
+ * 2, 3, 5, or above 2^26: pffft.c:1236-1277) -- the output array is then left
+ * untouched.  Every length pffft takes is served: powers of two 64 .. 2^20 by a cached
+ * streaming handle, the others (16, 32, 2^21 .. 2^26, mixed lengths) by a cached
+ * rfa_seam plan (rfa.h).  processIqBytesNative takes the handle's lengths only. */
 JNIEXPORT int rfa_jni_last_status(void);
 
 JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFT(JNIEnv *env, jobject thiz,

@@ -114,6 +114,15 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_windowed_fft_mag_planar": (ctypes.c_int, [_h, _fp, _fp, _fp, ctypes.c_size_t]),
         "rfa_fft_logmag_interleaved": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t]),
         "rfa_fft_ordered": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t]),
+        "rfa_seam_supported": (ctypes.c_int, [ctypes.c_int32]),
+        "rfa_seam_create": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(_h)]),
+        "rfa_seam_destroy": (ctypes.c_int, [_h]),
+        "rfa_seam_last_error": (ctypes.c_char_p, [_h]),
+        "rfa_seam_get_plan": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_int32)]),
+        "rfa_seam_windowed_fft_mag_planar": (ctypes.c_int, [_h, _fp, _fp, _fp, ctypes.c_size_t]),
+        "rfa_seam_fft_logmag_interleaved": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t]),
+        "rfa_seam_fft_ordered": (ctypes.c_int, [_h, _fp, _fp, ctypes.c_size_t]),
         "rfa_set_profiling": (ctypes.c_int, [_h, ctypes.c_int]),
         "rfa_get_kernel_time": (ctypes.c_int, [_h, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
         "rfa_main_kernel_name": (ctypes.c_char_p, [_h]),

@@ -3,8 +3,9 @@
 //
 // Reference behaviour kept: copy-in / copy-out through Get/SetFloatArrayRegion
 // (nativedsp.cpp:66,80), a cached per-size setup re-created on a size change
-// (nativedsp.cpp:56-64 -- here a handle, freed instead of leaked), no return
-// value on the legacy void symbols.  The new planar symbol returns JNI_FALSE on
+// (nativedsp.cpp:56-64 -- here a handle, freed instead of leaked; a mixed-radix
+// plan for the lengths pffft takes and the handle does not), no return value on
+// the legacy void symbols.  The new planar symbol returns JNI_FALSE on
 // a size mismatch like NativeDsp.kt:45-46.
 #include <cstring>
 #include <mutex>
@@ -58,6 +59,32 @@ rfa_handle *handle_for(int n, int fmt, int window) {
     return h;
 }
 
+// Lengths the handle does not take but pffft does (16, 32, 2^21 .. 2^26, mixed
+// 2/3/5 lengths) go to one cached plan, re-made on a size change like the
+// reference's single setup (nativedsp.cpp:26-33).
+rfa_seam *g_seam = nullptr;
+int g_seam_n = 0;
+
+rfa_seam *seam_for(int n) {
+    if (g_seam && g_seam_n == n) return g_seam;
+    if (g_seam) rfa_seam_destroy(g_seam);
+    g_seam = nullptr;
+    g_seam_n = 0;
+    g_status = rfa_seam_create(n, 0, &g_seam);
+    if (g_status != RFA_OK) return g_seam = nullptr;
+    g_seam_n = n;
+    return g_seam;
+}
+
+// the streaming handle for (n, fmt, window) when rfa_create takes n, else nullptr
+// and, for a length only pffft-style plans take, *seam
+rfa_handle *legacy_target(int n, int fmt, int window, rfa_seam **seam) {
+    *seam = nullptr;
+    if (rfa_handle *h = handle_for(n, fmt, window)) return h;
+    if (g_status == RFA_ERR_UNSUPPORTED && rfa_seam_supported(n)) *seam = seam_for(n);
+    return nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -75,11 +102,14 @@ JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFT(JNIEnv 
     std::lock_guard<std::mutex> lock(g_mu);
     g_status = RFA_ERR_UNSUPPORTED;
     if (length <= 0 || (length & 1)) return;
-    rfa_handle *h = handle_for(length / 2, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE);
-    if (!h) return;
+    rfa_seam *sp = nullptr;
+    rfa_handle *h = legacy_target(length / 2, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE, &sp);
+    if (!h && !sp) return;
     std::vector<float> in(length), out(length);
     (*env)->GetFloatArrayRegion(env, input, 0, length, in.data());
-    if ((g_status = rfa_fft_ordered(h, in.data(), out.data(), (size_t)length / 2)) != RFA_OK) return;
+    g_status = h ? rfa_fft_ordered(h, in.data(), out.data(), (size_t)length / 2)
+                 : rfa_seam_fft_ordered(sp, in.data(), out.data(), (size_t)length / 2);
+    if (g_status != RFA_OK) return;
     (*env)->SetFloatArrayRegion(env, output, 0, length, out.data());
 }
 
@@ -91,11 +121,14 @@ JNIEXPORT void JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performFFTAndLogMa
     g_status = RFA_ERR_UNSUPPORTED;
     if (length <= 0 || (length & 1)) return;
     const jsize out_len = length / 2;
-    rfa_handle *h = handle_for(out_len, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE);
-    if (!h) return;
+    rfa_seam *sp = nullptr;
+    rfa_handle *h = legacy_target(out_len, RFA_IN_F32_INTERLEAVED, RFA_WINDOW_NONE, &sp);
+    if (!h && !sp) return;
     std::vector<float> in(length), mag(out_len);
     (*env)->GetFloatArrayRegion(env, input, 0, length, in.data());
-    if ((g_status = rfa_fft_logmag_interleaved(h, in.data(), mag.data(), (size_t)out_len)) != RFA_OK) return;
+    g_status = h ? rfa_fft_logmag_interleaved(h, in.data(), mag.data(), (size_t)out_len)
+                 : rfa_seam_fft_logmag_interleaved(sp, in.data(), mag.data(), (size_t)out_len);
+    if (g_status != RFA_OK) return;
     (*env)->SetFloatArrayRegion(env, output, 0, out_len, mag.data());
 }
 
@@ -108,12 +141,15 @@ JNIEXPORT jboolean JNICALL Java_com_mantz_1it_nativedsp_NativeDsp_performWindowe
         return JNI_FALSE;
     }
     std::lock_guard<std::mutex> lock(g_mu);
-    rfa_handle *h = handle_for(n, RFA_IN_F32_PLANAR, RFA_WINDOW_BLACKMAN);
-    if (!h) return JNI_FALSE;
+    rfa_seam *sp = nullptr;
+    rfa_handle *h = legacy_target(n, RFA_IN_F32_PLANAR, RFA_WINDOW_BLACKMAN, &sp);
+    if (!h && !sp) return JNI_FALSE;
     std::vector<float> r(n), i(n), m(n);
     (*env)->GetFloatArrayRegion(env, re, 0, n, r.data());
     (*env)->GetFloatArrayRegion(env, im, 0, n, i.data());
-    if ((g_status = rfa_windowed_fft_mag_planar(h, r.data(), i.data(), m.data(), (size_t)n)) != RFA_OK) return JNI_FALSE;
+    g_status = h ? rfa_windowed_fft_mag_planar(h, r.data(), i.data(), m.data(), (size_t)n)
+                 : rfa_seam_windowed_fft_mag_planar(sp, r.data(), i.data(), m.data(), (size_t)n);
+    if (g_status != RFA_OK) return JNI_FALSE;
     (*env)->SetFloatArrayRegion(env, mag_out, 0, n, m.data());
     return JNI_TRUE;
 }

@@ -310,3 +310,77 @@ class SpectrumEngine:
         self._check(_lib.lib().rfa_get_kernel_time(self._h, ctypes.byref(ms), ctypes.byref(n)),
                     "rfa_get_kernel_time")
         return ms.value, n.value
+
+
+def seam_supported(n: int) -> bool:
+    """True when the reference's pffft accepts N (pffft.c:1231-1280): a multiple of 16,
+    N / 4 a product of 2, 3, 4, 5, N <= 2^26."""
+    return bool(_lib.lib().rfa_seam_supported(int(n)))
+
+
+class SeamPlan:
+    """The reference seams at one length the streaming handle does not take (16, 32,
+    2^21 .. 2^26, mixed 2/3/5 lengths): librfa's mixed-radix Stockham FFT on the GPU
+    (csrc/fft_seam.hip), one plan per N like nativedsp.cpp:12-17's cached setup."""
+
+    def __init__(self, n: int, device: int = 0):
+        h = ctypes.c_void_p()
+        check(_lib.lib().rfa_seam_create(int(n), int(device), ctypes.byref(h)), "rfa_seam_create")
+        self._h = h
+        self.n = int(n)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().rfa_seam_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _check(self, status: int, where: str) -> None:
+        if status != _lib.RFA_OK:
+            raise _lib.RfaError(status, where, (_lib.lib().rfa_seam_last_error(self._h) or b"").decode())
+
+    def plan(self) -> list[int]:
+        """Pass radices, first pass first."""
+        radices = (ctypes.c_int32 * 32)()
+        cnt = ctypes.c_int32()
+        self._check(_lib.lib().rfa_seam_get_plan(self._h, radices, 32, ctypes.byref(cnt)), "rfa_seam_get_plan")
+        return list(radices[: cnt.value])
+
+    def windowed_fft_mag(self, re: np.ndarray, im: np.ndarray, mag_out: np.ndarray) -> bool:
+        """NativeDsp.performWindowedFftAndReturnMag (NativeDsp.kt:43-62)."""
+        re = np.ascontiguousarray(re, np.float32)
+        im = np.ascontiguousarray(im, np.float32)
+        if im.size != re.size or mag_out.size != re.size:
+            return False
+        rc = _lib.lib().rfa_seam_windowed_fft_mag_planar(self._h, _fptr(re), _fptr(im), _fptr(mag_out), re.size)
+        if rc == _lib.RFA_ERR_SIZE:
+            return False
+        self._check(rc, "rfa_seam_windowed_fft_mag_planar")
+        return True
+
+    def fft_logmag(self, interleaved: np.ndarray) -> np.ndarray:
+        """JNI performFFTAndLogMag (nativedsp.cpp:44-81)."""
+        x = np.ascontiguousarray(interleaved, np.float32)
+        out = np.empty(x.size // 2, np.float32)
+        self._check(_lib.lib().rfa_seam_fft_logmag_interleaved(self._h, _fptr(x), _fptr(out), out.size),
+                    "rfa_seam_fft_logmag_interleaved")
+        return out
+
+    def fft_ordered(self, interleaved: np.ndarray) -> np.ndarray:
+        """JNI performFFT (nativedsp.cpp:19-42)."""
+        x = np.ascontiguousarray(interleaved, np.float32)
+        out = np.empty_like(x)
+        self._check(_lib.lib().rfa_seam_fft_ordered(self._h, _fptr(x), _fptr(out), x.size // 2),
+                    "rfa_seam_fft_ordered")
+        return out

@@ -10,13 +10,21 @@ Same method names, argument meaning and error behaviour:
 * ``performFFTAndLogMag(input, output)`` / ``performFFT(input, output)``
   (the two ``external`` natives, NativeDsp.kt:27-28 -> nativedsp.cpp:19-81).
 
+Every length the reference's pffft accepts works: powers of two from 64 to 2^20
+run on a streaming handle's fused kernels, the rest (16, 32, 2^21 .. 2^26, mixed
+2/3/5 lengths) on a mixed-radix plan (``engine.SeamPlan``).  A length pffft
+rejects raises ``RfaError`` (RFA_ERR_UNSUPPORTED) where the reference asserts.
+
 Like the reference (NativeDsp.kt:23-26) one instance is meant for one thread.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from .engine import SpectrumEngine
+from .engine import SeamPlan, SpectrumEngine
+
+# lengths rfa_create takes (include/rfa.h RFA_MIN_FFT_SIZE .. RFA_MAX_FFT_SIZE, powers of two)
+_HANDLE_MIN, _HANDLE_MAX = 64, 1 << 20
 
 
 class NativeDsp:
@@ -25,18 +33,26 @@ class NativeDsp:
         self._planar = None  # Blackman, f32 planar
         self._raw = None     # no window, f32 interleaved
 
-    def _engine(self, kind: str, n: int) -> SpectrumEngine:
+    def _engine(self, kind: str, n: int) -> SpectrumEngine | SeamPlan:
         cur = self._planar if kind == "planar" else self._raw
         if cur is None or cur.n != n:  # nativedsp.cpp:56-64: new setup on a size change
             if cur is not None:
                 cur.close()
-            if kind == "planar":
+            self._set(kind, None)
+            if not (_HANDLE_MIN <= n <= _HANDLE_MAX and n & (n - 1) == 0):
+                cur = SeamPlan(n, device=self.device)
+            elif kind == "planar":
                 cur = SpectrumEngine(n, "blackman", "f32p", ring_rows=0, device=self.device)
-                self._planar = cur
             else:
                 cur = SpectrumEngine(n, "none", "f32", ring_rows=0, device=self.device)
-                self._raw = cur
+            self._set(kind, cur)
         return cur
+
+    def _set(self, kind: str, obj) -> None:
+        if kind == "planar":
+            self._planar = obj
+        else:
+            self._raw = obj
 
     def performWindowedFftAndReturnMag(self, re, im, magOut) -> bool:  # noqa: N802,N803 - reference name
         n = len(re)

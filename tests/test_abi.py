@@ -129,3 +129,27 @@ def test_product_library_ships_only_the_wide_64k_kernel(lib):
         blob = fh.read()
     assert b"fft64_kernel" not in blob
     assert b"fft_wide_kernel" in blob
+
+
+def _pffft_accepts(n: int) -> bool:
+    """pffft_new_setup(N, PFFFT_COMPLEX) (pffft.c:1231-1280) succeeds: 0 < N <= 2^26,
+    N % 16 == 0, and decompose() of N / 4 over {5, 3, 4, 2} leaves nothing."""
+    if n <= 0 or n > (1 << 26) or n % 16:
+        return False
+    m = n // 4
+    for f in (5, 3, 4, 2):
+        while m % f == 0:
+            m //= f
+    return m == 1
+
+
+def test_seam_length_rule_matches_pffft(lib):
+    """rfa_seam_supported (host only, no device) takes exactly pffft's lengths."""
+    lib.rfa_seam_supported.restype = ctypes.c_int
+    lib.rfa_seam_supported.argtypes = [ctypes.c_int32]
+    sizes = list(range(-16, 20000)) + [3 << 20, 5 << 20, 15 << 22, 1 << 26, (1 << 26) + 16, 1 << 27, 2 ** 31 - 1]
+    bad = [n for n in sizes if bool(lib.rfa_seam_supported(n)) != _pffft_accepts(n)]
+    assert not bad, bad[:10]
+    h = ctypes.c_void_p()
+    assert lib.rfa_seam_create(1000, 0, ctypes.byref(h)) == -3 and not h.value  # unsupported, checked first
+    assert lib.rfa_seam_destroy(None) == -1

@@ -202,12 +202,13 @@ def test_legacy_calls_alternate_without_losing_the_partial_frame(rfa):
     assert gu.db_diff(np.stack(rows), exp) <= gu.DB_TOL
 
 
-@pytest.mark.parametrize("m", [48, 480, 16, 32])
+@pytest.mark.parametrize("m", [8, 40, 112, 1000])
 def test_legacy_unsupported_length_reports_status(rfa, m):
-    """Lengths the reference's pffft takes (a multiple of 16 with factors 2, 3, 5:
-    pffft.c:1236-1247) but librfa does not (powers of two from 64): the void legacy
-    symbol leaves its output untouched and rfa_jni_last_status() says
-    RFA_ERR_UNSUPPORTED; the next supported call resets it to RFA_OK."""
+    """Lengths the reference's pffft rejects (not a multiple of 16, or a factor other
+    than 2, 3, 5: pffft.c:1236-1277, where the reference asserts or gets a null setup):
+    the void legacy symbol leaves its output untouched and rfa_jni_last_status() says
+    RFA_ERR_UNSUPPORTED; the next supported call resets it to RFA_OK.  (Every length
+    pffft takes is served: tests/test_gpu_seam.py.)"""
     jenv = MockJNIEnv()
     status = rfa.lib().rfa_jni_last_status
     status.restype = _I32
