@@ -9,6 +9,7 @@ reference's interfaces for this path:
     processor.FftProcessor     analyzer/FftProcessor.kt
     source.FileIQSource        source/FileIQSource.java (+ Scheduler framing)
     engine.SpectrumEngine      one librfa handle
+    engine.SeamPlan            the legacy seams at pffft-only lengths (mixed 2/3/5, 16, 32, > 2^20)
     SpectrumEngine.draw_preprocess, scanner   AnalyzerSurface.drawPreprocessing, MainViewModel scanner
     recording                  Scheduler recording branch, file names, replay metadata
     demod.FrontEnd             IQConverter.mixPacketIntoSamplePacket + Decimator / Resampler
@@ -17,6 +18,6 @@ reference's interfaces for this path:
 There is no CPU fallback: without librfa.so or a HIP device, calls raise.
 """
 from ._lib import RfaError, build, device_count, lib  # noqa: F401
-from .engine import SpectrumEngine  # noqa: F401
+from .engine import SeamPlan, SpectrumEngine  # noqa: F401
 
-__all__ = ["SpectrumEngine", "RfaError", "build", "device_count", "lib"]
+__all__ = ["SpectrumEngine", "SeamPlan", "RfaError", "build", "device_count", "lib"]
