@@ -40,8 +40,8 @@ rfa_handle *handle_for(int n, int fmt, int window) {
         }
         if (!s.h || (victim->h && s.used < victim->used)) victim = &s;
     }
-    if (victim->h) rfa_destroy(victim->h);
-    *victim = Setup();
+    // a length or format the handle refuses evicts nothing: a cached setup's pending
+    // partial frame survives any call in between
     rfa_config c;
     rfa_default_config(&c);
     c.fft_size = n;
@@ -49,8 +49,10 @@ rfa_handle *handle_for(int n, int fmt, int window) {
     c.window = window;
     c.ring_rows = 0;
     rfa_handle *h = nullptr;
-    g_status = rfa_create(&c, &h);  // e.g. RFA_ERR_UNSUPPORTED for a length pffft takes and librfa does not
+    g_status = rfa_create(&c, &h);  // e.g. RFA_ERR_UNSUPPORTED for a length only a seam plan takes
     if (g_status != RFA_OK) return nullptr;
+    if (victim->h) rfa_destroy(victim->h);
+    *victim = Setup();
     victim->h = h;
     victim->n = n;
     victim->fmt = fmt;
@@ -60,20 +62,33 @@ rfa_handle *handle_for(int n, int fmt, int window) {
 }
 
 // Lengths the handle does not take but pffft does (16, 32, 2^21 .. 2^26, mixed
-// 2/3/5 lengths) go to one cached plan, re-made on a size change like the
-// reference's single setup (nativedsp.cpp:26-33).
-rfa_seam *g_seam = nullptr;
-int g_seam_n = 0;
+// 2/3/5 lengths) go to cached plans keyed by N (nativedsp.cpp:26-33 keeps one
+// setup; two slots here, so alternating two such lengths does not rebuild).
+constexpr int kSeamSlots = 2;
+struct SeamSlot {
+    rfa_seam *s = nullptr;
+    int n = 0;
+    unsigned long long used = 0;
+};
+SeamSlot g_seams[kSeamSlots];
 
 rfa_seam *seam_for(int n) {
-    if (g_seam && g_seam_n == n) return g_seam;
-    if (g_seam) rfa_seam_destroy(g_seam);
-    g_seam = nullptr;
-    g_seam_n = 0;
-    g_status = rfa_seam_create(n, 0, &g_seam);
-    if (g_status != RFA_OK) return g_seam = nullptr;
-    g_seam_n = n;
-    return g_seam;
+    SeamSlot *victim = &g_seams[0];
+    for (SeamSlot &e : g_seams) {
+        if (e.s && e.n == n) {
+            e.used = ++g_tick;
+            return e.s;
+        }
+        if (!e.s || (victim->s && e.used < victim->used)) victim = &e;
+    }
+    rfa_seam *s = nullptr;
+    g_status = rfa_seam_create(n, 0, &s);
+    if (g_status != RFA_OK) return nullptr;
+    if (victim->s) rfa_seam_destroy(victim->s);
+    victim->s = s;
+    victim->n = n;
+    victim->used = ++g_tick;
+    return s;
 }
 
 // the streaming handle for (n, fmt, window) when rfa_create takes n, else nullptr

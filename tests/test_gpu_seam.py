@@ -164,3 +164,51 @@ def test_jni_legacy_symbols_at_pffft_only_lengths(rfa, m):
         assert gu.pffft_diff(mag, oracle.ref_fft_logmag(x)) <= gu.DB_TOL
         w = oracle.window(m, oracle.WIN_BLACKMAN)
         assert gu.pffft_diff(wmag, oracle.ref_fft_logmag(oracle.windowed_interleaved(re, im, w))) <= gu.DB_TOL
+
+
+def test_seam_and_refused_lengths_keep_the_framing_setup(rfa):
+    """A legacy call at a length the handle does not take (a seam plan's 48 or 2^21, or
+    1000, which pffft rejects too) evicts no cached handle: with the shim's four slots
+    full and the framing-mode setup the least recently used, processIqBytesNative's
+    partial frame survives them, and every row of the reference framing arrives."""
+    from oracle import processor
+    import signals
+    n, pkt = 8192, 1500
+    jenv = MockJNIEnv()
+    lib = rfa.lib()
+    status = lib.rfa_jni_last_status
+    status.restype = ctypes.c_int32
+    frame_fn = getattr(lib, _P + "processIqBytesNative")
+    frame_fn.restype = ctypes.c_int32
+    frame_fn.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int32] * 3 + [ctypes.c_void_p]
+    fft = getattr(lib, _P + "performFFT")
+    logmag = getattr(lib, _P + "performFFTAndLogMag")
+    for fn in (fft, logmag):
+        fn.restype = None
+        fn.argtypes = [ctypes.c_void_p] * 4
+
+    def legacy(fn, m):
+        fn(jenv.env, None, jenv.new_array(np.ones(2 * m, np.float32)), jenv.new_array(np.zeros(2 * m, np.float32)))
+        return status()
+
+    for m in (64, 128, 256, 512):  # fill the four slots: no framing setup of an earlier test survives
+        assert legacy(fft, m) == 0
+    raw = signals.frames_bytes(n, 4, "u8", 23, tones=((0.17, 0.5),), noise=0.04)
+    packets = [raw[i:i + pkt] for i in range(0, len(raw) - pkt + 1, pkt)]
+    frames = processor.scheduler_frames([(b, 0, 1) for b in packets], n, 2)
+    rows = []
+    for b in packets:
+        out = np.zeros(n, np.float32)
+        got = frame_fn(jenv.env, None, jenv.new_array(np.frombuffer(b, np.int8).copy()), 1, n, 0,
+                       jenv.new_array(out))  # format 1 = u8
+        assert got in (0, 1) and status() == 0
+        if got:
+            rows.append(out)
+        for m in (128, 256, 512):  # the framing setup is now the least recently used slot
+            assert legacy(fft, m) == 0
+        assert legacy(fft, 48) == 0
+        assert legacy(logmag, 1 << 21) == 0
+        assert legacy(fft, 1000) == -3
+    assert len(rows) == len(frames) > 0
+    exp = np.stack([oracle.spectrum_rows(f[0], oracle.IN_U8, n, 1, None, oracle.WIN_BLACKMAN)[0] for f in frames])
+    assert gu.db_diff(np.stack(rows), exp) <= gu.DB_TOL
