@@ -950,6 +950,14 @@ static hipError_t wide_by_fmt(const FftLaunch &a) {
 
 bool wide_supported(int logn) { return logn >= 13 && logn <= 17; }
 
+#ifndef RFA_AB_BUILD
+// The wave-decoupled 64 K kernel (scripts/ab/fft_w64.hip, 8-10 % slower: profiles/r04/w64_ab.txt)
+// is linked into A/B builds only; product builds run the wide kernel for every 64 K format.
+bool w64_format(int) { return false; }
+std::vector<float2> w64_twiddles() { return {}; }
+hipError_t launch_fft64(const FftLaunch &) { return hipErrorInvalidValue; }
+#endif
+
 // Twiddle blob for the wide kernel (layout must match WGeo): pass-1 [32][R1-1],
 // pass-2 A [TPF/LO][15] (none at 8 K: WGeo::A_ALIAS), B [LO][15], pre-stage pre_a [RS][M/32], pre_b [RS][32].
 std::vector<float2> wide_twiddles(int logn, int pt, int lm) {

@@ -32,8 +32,8 @@
 #include <type_traits>
 #include <vector>
 
-#include "fft_common.h"
-#include "fft_kernels.h"
+#include "../../rfanalyzer_amd/csrc/fft_common.h"
+#include "../../rfanalyzer_amd/csrc/fft_kernels.h"
 
 namespace rfa {
 namespace {

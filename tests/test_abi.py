@@ -122,7 +122,7 @@ def test_product_library_reads_no_environment(lib):
 
 def test_product_library_ships_only_the_wide_64k_kernel(lib):
     """N = 64 K runs the wide kernel in product builds: the wave-decoupled kernel
-    (fft_w64.hip, measured 8-10 % slower, profiles/r04/w64_ab.txt) is compiled into A/B
+    (scripts/ab/fft_w64.hip, measured 8-10 % slower, profiles/r04/w64_ab.txt) is linked into A/B
     builds only, so its code object is absent from the product librfa.so."""
     from rfanalyzer_amd import _lib
     with open(_lib.LIB_PATH, "rb") as fh:
