@@ -27,7 +27,10 @@ Companions on the same line (never ``value``), run by every rank in multi-GPU
 runs with per-rank times: ``f32`` (the headline on float32 IQ), ``config2``
 (16 K cf32 Hann), ``config4`` / ``config4_f32`` (the shard workload on s8 and cf32
 input), ``config5`` (a 1 M-point
-stream per rank), ``demod`` and, on rank 0 of a 1-GPU run, ``cpu_baseline``.
+stream per rank), ``host_fed`` (configs 3 and 2 fed from pinned host memory over
+PCIe, H2D overlapped on a second stream), ``demod`` and, on rank 0 of a 1-GPU run,
+``cpu_baseline`` and ``config4.one_batch_per_call.c_loop`` (tools/call_bench: the
+C-ABI's per-call cost timed from C).
 
 Launch: ``python bench.py --gpus N`` spawns N ranks itself (one process per
 GPU, started before anything touches the GPU, 127.0.0.1 rendezvous); under
@@ -85,6 +88,8 @@ def parse(argv=None):
     p.add_argument("--c4-steps", type=int, default=3, help="steps of the 256 x 8192 shard (config 4) companion (0 = skip)")
     p.add_argument("--demod-steps", type=int, default=5,
                    help="calls of the demod front-end companion (SURVEY §8(f) row 4; 0 = skip)")
+    p.add_argument("--host-fed-calls", type=int, default=40,
+                   help="calls of the host-fed companions (pinned host IQ, H2D overlapped; 0 = skip)")
     p.add_argument("--profile-every", type=int, default=8,
                    help="HIP-event timing of every K-th main-kernel launch in the timed region (1 = all)")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -367,6 +372,83 @@ def demod_companion(torch, device, steps, samples=1 << 26):
     return {"workload": "u8 2.4 Msps -> 96 kHz, mix + 273-tap decimating FIR (D 25)", "value": round(samples / dt / 1e6, 1),
             "unit": "Msamples/s", "ms_per_call": round(dt * 1e3, 4), "samples_per_call": samples, "decimation": d,
             "taps": t}
+
+
+def host_fed_run(torch, device, n, fmt, frames, calls, window="blackman", avg="ema", peak=True, ring_rows=500,
+                 host_batches=2, seed=7):
+    """Host-fed end to end (SURVEY.md §7 "Host feed vs device throughput"; the reference path
+    is host-fed by construction: FileIQSource.java:318-369 -> Scheduler.kt:252-279 ->
+    FftProcessor.kt:111-140).  The raw IQ batches sit in pinned host memory; each call's batch
+    is copied H2D on a second stream into one of two device buffers (double buffering: the
+    copy of batch i+1 runs while batch i is processed), then rfa_process() reads it into the
+    device ring + peak / EMA state only (no rows back).  Returns wall-clock Msamples/s over
+    `calls` calls, the H2D-only rate of the same copies, and the per-call split."""
+    import rfanalyzer_amd
+
+    st = torch.cuda.current_stream(device)
+    cp = torch.cuda.Stream(device)
+    eng = rfanalyzer_amd.SpectrumEngine(n, window, fmt, avg=avg, avg_length=min(30, ring_rows - 1), ema_alpha=0.1,
+                                        peak_hold=peak, ring_rows=ring_rows, device=device.index or 0)
+    eng.set_stream(st.cuda_stream)
+    eng.set_tuning(100_000_000, 20_000_000)
+    src = make_pool(torch, n, frames, fmt, 1, seed, device)[:host_batches]  # synthetic batches, made on device
+    host = [b.view(torch.uint8).cpu().pin_memory() for b in src]
+    del src
+    nbytes = host[0].numel()
+    dev = [torch.empty(nbytes, dtype=torch.uint8, device=device) for _ in range(2)]
+    ready = [torch.cuda.Event() for _ in range(2)]
+    done = [torch.cuda.Event() for _ in range(2)]
+    for e in done:
+        e.record(st)
+
+    def run(k_calls, process=True):
+        for i in range(k_calls):
+            j = i & 1
+            with torch.cuda.stream(cp):
+                cp.wait_event(done[j])  # the batch that last used this buffer has been read
+                dev[j].copy_(host[i % len(host)], non_blocking=True)
+                ready[j].record(cp)
+            if process:
+                st.wait_event(ready[j])
+                eng.process_device(dev[j].data_ptr(), frames, 0, None)
+                done[j].record(st)
+            else:
+                done[j].record(cp)
+
+    run(4)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    run(calls)
+    torch.cuda.synchronize(device)
+    el = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    run(calls, process=False)
+    torch.cuda.synchronize(device)
+    el_copy = time.perf_counter() - t0
+    eng.close()
+    samples = calls * frames * n
+    return {"value": round(samples / el / 1e6, 2), "unit": "Msamples/s", "ms_per_call": round(el / calls * 1e3, 4),
+            "h2d_GBps": round(calls * nbytes / el_copy / 1e9, 2),
+            "h2d_only_ms_per_call": round(el_copy / calls * 1e3, 4), "bytes_per_call": nbytes,
+            "frames_per_call": frames, "calls": calls}
+
+
+def c_call_cost(calls=4000):
+    """tools/call_bench (built by __graft_entry__.build()): the C-ABI's per-call cost for
+    config 4's 256 x 8192 s8 batches timed from a C loop (no Python / ctypes), one batch per
+    rfa_process_batches call and 64 per call.  None when the binary is absent."""
+    exe = os.path.join(ROOT, "tools", "call_bench")
+    if not os.path.exists(exe):
+        return None
+    out = {}
+    for kb in (1, 64):
+        r = subprocess.run([exe, str(calls if kb == 1 else max(1, calls // 64)), str(kb)], capture_output=True,
+                           text=True, timeout=300)
+        if r.returncode != 0:
+            out[f"batches_per_call_{kb}"] = {"error": (r.stderr or r.stdout)[-300:]}
+            continue
+        out[f"batches_per_call_{kb}"] = json.loads(r.stdout.strip().splitlines()[-1])
+    return out
 
 
 def pmc_traffic(args, fmt, n, frames):
@@ -794,6 +876,29 @@ def companions(args, ranks, result):
                              **_roof(a.frames * a.fft_size * (BPS[fmt] + 4), k),
                              "note": "kernel_ms = the whole large-N launch (front kernel + 32 K kernel B)"}
         result["config5"]["realtime_headroom"] = round(result["config5"]["value"] / W / 250.0, 1)  # 250 Msps streams
+    if args.host_fed_calls > 0 and not args.dry_run:
+        # the headline is device-resident; the host-fed end-to-end rate is reported
+        # beside it (never `value`).  Every rank feeds its own GPU over its own PCIe link.
+        torch = ranks.torch
+        hf3 = host_fed_run(torch, ranks.device, n, fmt, args.frames, args.host_fed_calls, window=args.window,
+                           avg=args.avg, peak=not args.no_peak, ring_rows=args.ring_rows)
+        hf2 = host_fed_run(torch, ranks.device, 16384, "f32", 1024, max(4, args.host_fed_calls // 2), window="hann",
+                           avg="none", peak=False, ring_rows=500)
+        v3, v2 = ranks.all_values(hf3["value"]), ranks.all_values(hf2["value"])
+        result["host_fed"] = {
+            "note": "pinned host IQ -> H2D on a second stream (double-buffered, overlapped with the previous "
+                    "batch's kernels) -> rfa_process into the device ring + state, no rows back; wall clock; "
+                    "PCIe-bound, never `value`",
+            "config3": dict(hf3, workload=f"config3 host-fed: {n}-pt {args.window}, {fmt} IQ, {args.avg} + peak-hold, "
+                                          f"ring {args.ring_rows}, {args.frames} frames per call",
+                            value=round(sum(v3), 2), per_rank_value=v3,
+                            device_resident_ratio=round(result.get("value", 0) / max(sum(v3), 1e-9), 2)
+                            if "value" in result else None),
+            "config2": dict(hf2, workload="config2 host-fed: 16384-pt Hann, cf32 IQ, ring 500, 1024 frames per call",
+                            value=round(sum(v2), 2), per_rank_value=v2,
+                            realtime_headroom_vs_20msps=round(min(v2) / 20.0, 1))}
+    if ranks.rank == 0 and ranks.world == 1 and args.c4_steps > 0 and not args.dry_run and "config4" in result:
+        result["config4"]["one_batch_per_call"]["c_loop"] = c_call_cost()
     if ranks.rank == 0 and args.demod_steps > 0 and not args.dry_run:
         result["demod"] = demod_companion(ranks.torch, ranks.device, args.demod_steps)
 

@@ -568,6 +568,20 @@ __device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, i
     __builtin_amdgcn_raw_buffer_store_b64(v, rs, voff, soff, 0);
 }
 
+// One frame of a chunk's peak / EMA summary (the chunked scan of fft_kernels.hip
+// state_partial_kernel: pk = max, emi = the EMA started from -inf, b = the affine offset
+// of the EMA started from 0, restart = some frame was -inf).  Peak: FftProcessor.kt:241-242;
+// EMA (extension): the avg += alpha (x - avg) idiom of GlobalPerformanceData.kt:44-50.
+// Explicit fmaf: every kernel that forms a summary (state_partial / state_fused and the
+// wide kernel's in-grid units) rounds identically, so the result does not depend on
+// which of them computed a chunk.
+RFA_HD void state_step(float &pk, float &emi, float &b, bool &restart, float x, float al) {
+    pk = fmaxf(pk, x);
+    emi = (emi > -INFINITY) ? fmaf(al, x - emi, emi) : x;
+    restart |= x == -INFINITY;
+    b = fmaf(al, x - b, b);
+}
+
 // Row value 10*log10(sqrt((Re/N)^2 + (Im/N)^2)) (nativedsp.cpp:73-78) from the
 // UNSCALED FFT output x.  Scaling by 1/N is exact (power of two), so the power
 // is (x.x^2 + x.y^2) * 2^(-2 log2 N) and the dB value is

@@ -508,13 +508,7 @@ __global__ void state_partial_kernel(StateLaunch a, int chunk_len) {
         const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
         const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float x = xs[k];
-            pk[k] = fmaxf(pk[k], x);
-            emi[k] = (emi[k] > -INFINITY) ? emi[k] + al * (x - emi[k]) : x;
-            restart[k] |= x == -INFINITY;
-            b[k] = b[k] + al * (x - b[k]);
-        }
+        for (int k = 0; k < 4; k++) state_step(pk[k], emi[k], b[k], restart[k], xs[k], al);
         am *= keep;
     }
     float4 *out = a.part + (size_t)c * a.n + bin;
@@ -547,29 +541,31 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     __shared__ float4 part[CH][BPB];
     const int c = threadIdx.x / TPC, l = threadIdx.x % TPC;
     const int bin = blockIdx.x * BPB + 4 * l;
-    const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
-    const float al = a.ema_alpha, keep = 1.0f - al;
-    float pk[4], emi[4], b[4];
-    bool restart[4];
+    if (a.cnt && blockIdx.x == 0 && threadIdx.x <= kStMaxChunks) a.cnt[threadIdx.x] = 0u;  // in-grid counters
+    // chunk c of this block's bins summarised in-grid by the main kernel (FftLaunch st_*):
+    // the same float4 state_step forms, so which kernel formed it does not change the result
+    if (a.done && a.done[c * (a.n / kStRange) + blockIdx.x * BPB / kStRange] == a.gen) {
 #pragma unroll
-    for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
-    float am = 1.0f;
+        for (int k = 0; k < 4; k++) part[c][4 * l + k] = a.part[(size_t)c * a.n + bin + k];
+    } else {
+        const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
+        const float al = a.ema_alpha, keep = 1.0f - al;
+        float pk[4], emi[4], b[4];
+        bool restart[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
+        float am = 1.0f;
 #pragma unroll 4  // frames in flight per thread (profiles/r02c/state_unroll_ab.txt)
-    for (int f = f0; f < f1; f++) {
-        const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
-        const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+        for (int f = f0; f < f1; f++) {
+            const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
+            const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float x = xs[k];
-            pk[k] = fmaxf(pk[k], x);
-            emi[k] = (emi[k] > -INFINITY) ? emi[k] + al * (x - emi[k]) : x;
-            restart[k] |= x == -INFINITY;
-            b[k] = b[k] + al * (x - b[k]);
+            for (int k = 0; k < 4; k++) state_step(pk[k], emi[k], b[k], restart[k], xs[k], al);
+            am *= keep;
         }
-        am *= keep;
-    }
 #pragma unroll
-    for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
+        for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);
+    }
     __syncthreads();
     const int lr = state_logrs(a), lm = ring_logm(lr, ilog2_dev(a.n));
     for (int i = threadIdx.x; i < BPB; i += 256) {
@@ -593,6 +589,16 @@ static const bool kStateTileOff = std::getenv("RFA_STATE_TILE") && std::atoi(std
 static constexpr bool kStateTileOff = false;
 #endif
 
+bool state_fused_plan(int n, int n_frames, int max_chunks, int fused, int *chunks, int *chunk_len) {
+    const int c = std::min(max_chunks, (n_frames + 7) / 8);
+    if (c < 8 || !fused) return false;
+    const int ch = c >= 32 ? 32 : c >= 16 ? 16 : 8;
+    if (n % (1024 / ch)) return false;
+    *chunks = ch;
+    *chunk_len = (n_frames + ch - 1) / ch;
+    return true;
+}
+
 hipError_t launch_state(const StateLaunch &a) {
     if (a.n_frames <= 0) return hipSuccess;
     const int tpb = 256;
@@ -608,16 +614,14 @@ hipError_t launch_state(const StateLaunch &a) {
     }
     const int bx = (a.n + tpb - 1) / tpb;
     int chunks = a.part ? std::min(a.max_chunks, (a.n_frames + 7) / 8) : 1;
-    if (chunks >= 8 && a.fused) {  // single-launch form: CH = 8, 16 or 32 chunks
-        const int ch = chunks >= 32 ? 32 : chunks >= 16 ? 16 : 8;
-        const int bpb = 1024 / ch;
-        if (a.n % bpb == 0) {
-            const int len = (a.n_frames + ch - 1) / ch;
-            auto k = ch == 32 ? state_fused_kernel<32> : ch == 16 ? state_fused_kernel<16> : state_fused_kernel<8>;
-            hipLaunchKernelGGL(k, dim3(a.n / bpb), dim3(256), 0, a.stream, a, len);
-            return hipGetLastError();
-        }
+    int ch = 0, len = 0;
+    if (a.part && state_fused_plan(a.n, a.n_frames, a.max_chunks, a.fused, &ch, &len)) {
+        // single-launch form: CH = 8, 16 or 32 chunks (with a.done: also the in-grid fold)
+        auto k = ch == 32 ? state_fused_kernel<32> : ch == 16 ? state_fused_kernel<16> : state_fused_kernel<8>;
+        hipLaunchKernelGGL(k, dim3(a.n / (1024 / ch)), dim3(256), 0, a.stream, a, len);
+        return hipGetLastError();
     }
+    if (a.done) return hipErrorInvalidValue;  // in-grid summaries need the fused fold
     if (chunks > 1) {
         const int len = (a.n_frames + chunks - 1) / chunks;
         chunks = (a.n_frames + len - 1) / len;

@@ -28,6 +28,13 @@
 
 namespace rfa {
 
+// in-grid state (fft_wide_kernel IGS): sc1 cache policy of a raw buffer load (gfx950: bit 4 of
+// the aux operand; the load then bypasses the CU's L1), and how long a workgroup that has
+// finished its own items keeps polling for chunks still in flight (s_memrealtime ticks of
+// 10 ns) before it leaves the rest to the finish kernel
+constexpr int kSc1 = 16;
+constexpr unsigned long long kStWaitTicks = 4000;
+
 template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
@@ -592,6 +599,113 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // staged frame skips them -- vmcnt counts in issue order and they are younger
     // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
     int pending_st = 0;
+
+    // ---- in-grid peak / EMA state (FftLaunch st_*; 64 K staged kernels).
+    // A work item's ring stores are write-through (sc1); once every wave has drained them
+    // (vmcnt(0) before a workgroup barrier) one lane adds 1 to st_cnt[chunk of the frame]
+    // (agent scope).  Between items the workgroup takes a unit (chunk c, kStRange storage
+    // positions) of a COMPLETE chunk: the lane that saw the count polled it, the others pass a
+    // barrier after it, and every row load is an sc1 load (MI355X_MICROARCH.md, valid
+    // hand-off forms, row 1).  Nothing ever waits for another workgroup without a bound, so
+    // the grid cannot deadlock however many workgroups are resident; units nobody took are
+    // computed by state_fused_kernel (fft_kernels.hip), which also folds every summary.
+    constexpr bool IGS = STG && RS == 2 && LOGM == 15 && !COMPLEX_OUT && (DIAG & ~32) == 0;
+    // the st_* arguments are read through an opaque kernarg pointer where they are used, so
+    // hipcc cannot hoist them into registers held across the FFT (they pushed its SGPR spills
+    // 16 -> 104 and cost a VGPR spill when held)
+    // (readfirstlane: an inline-asm result counts as divergent, and descriptors built from
+    // divergent values would land in VGPRs where the store asm wants SGPRs)
+    using KArg = const __attribute__((address_space(4))) FftLaunch;
+    auto st_args = [] {
+        const unsigned long long p = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+        unsigned lo = (unsigned)p, hi = (unsigned)(p >> 32);
+        asm volatile("" : "+s"(lo), "+s"(hi));
+        lo = __builtin_amdgcn_readfirstlane(lo);
+        hi = __builtin_amdgcn_readfirstlane(hi);
+        return (KArg *)(((unsigned long long)hi << 32) | lo);
+    };
+    // re-read per use through the opaque pointer: a loop-invariant flag would let hipcc
+    // unswitch the item loop into two copies of the whole FFT (twice the code, 5x the spills)
+    auto igs_on = [&] {
+        if constexpr (!IGS) return false;
+        KArg *k = st_args();
+        return k->st_chunk_len > 0 && k->ring != nullptr && k->rows == nullptr;
+    };
+    int prev_chunk = -1;  // chunk of the previous item while its completion is not yet signalled
+    auto st_signal = [&] {  // after every wave's vmcnt(0) and a barrier
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(&st_args()->st_cnt[prev_chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        prev_chunk = -1;
+    };
+    auto run_unit = [&](int t) {
+        KArg *k = st_args();
+        constexpr int ranges = M * RS / kStRange;
+        const int c = t / ranges, pos = (t - c * ranges) * kStRange + (int)threadIdx.x;
+        const int cl = k->st_chunk_len, f0 = c * cl, nf = min(k->n_frames - f0, cl);
+        const int rows = k->ring_rows;
+        int rr = (k->ring_base - f0) % rows;
+        if (rr < 0) rr += rows;
+        const rsrc_t rs = make_rsrc(k->ring, (unsigned)rows * (unsigned)(n * 4));
+        // the row offset rides in the lane offset, one register stepped per frame: 32 uniform
+        // row offsets held at once would raise the kernel's SGPR pressure (and spill the FFT's)
+        unsigned voff = (unsigned)rr * (unsigned)(n * 4) + (unsigned)pos * 4u;
+        const unsigned wrap = (unsigned)rows * (unsigned)(n * 4);
+        float x[32];
+#pragma unroll
+        for (int j = 0; j < 32; j++) {  // every frame of the chunk in flight (sc1: written through by other CUs)
+            if (j < nf) x[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, 0, kSc1));
+            voff = rr == 0 ? voff + wrap - n * 4 : voff - n * 4;  // FftProcessor.kt:226-227: frame f + 1 one row earlier
+            rr = rr == 0 ? rows - 1 : rr - 1;
+        }
+        float pk = -INFINITY, emi = -INFINITY, b = 0.0f, am = 1.0f;
+        bool restart = false;
+        const float al = k->st_alpha, keep = 1.0f - al;
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            if (j < nf) {
+                state_step(pk, emi, b, restart, x[j], al);
+                am *= keep;
+            }
+        }
+        buf_store_f32x4(pk, restart ? -1.0f : am, b, emi, make_rsrc(k->st_part + (size_t)c * n, n * 16), pos * 16, 0);
+        if (threadIdx.x == 0) k->st_done[t] = k->st_gen;
+        pending_st = 0;  // the unit waited for its loads, so everything older (the staged frame) landed too
+    };
+    auto take_units = [&](int max_units) {
+        constexpr int ranges = M * RS / kStRange;
+        int *lds_slot = reinterpret_cast<int *>(lds + G::TW_LDS + G::SLOTS * G::HALFP);
+        for (int it = 0; max_units < 0 || it < max_units; it++) {
+            if (threadIdx.x == 0) {
+                KArg *k = st_args();
+                const int cl = k->st_chunk_len, nfr = k->n_frames;
+                const int total = ((nfr + cl - 1) / cl) * ranges;
+                unsigned *cnt = k->st_cnt, *tickets = cnt + kStMaxChunks;
+                auto ready = [&](unsigned t) {
+                    const int c = (int)t / ranges;
+                    const unsigned need = 2u * (unsigned)min(nfr - c * cl, cl);  // RS = 2 items per frame
+                    return __hip_atomic_load(&cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
+                };
+                const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + kStWaitTicks;
+                int unit = -1;  // -1: none (stop), >= 0: run it, -2: a ticket the finish kernel will serve
+                for (;;) {
+                    const unsigned t = __hip_atomic_load(tickets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if ((int)t >= total) break;
+                    if (ready(t)) {
+                        const unsigned mine = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((int)mine < total) unit = ready(mine) ? (int)mine : -2;
+                        break;
+                    }
+                    if (max_units >= 0 || __builtin_amdgcn_s_memrealtime() >= t_end) break;
+                    __builtin_amdgcn_s_sleep(16);
+                }
+                lds_slot[it & 1] = unit;
+            }
+            lds_barrier();
+            const int unit = __builtin_amdgcn_readfirstlane(lds_slot[it & 1]);  // uniform: descriptors in SGPRs
+            if (unit == -1) break;
+            if (unit >= 0) run_unit(unit);
+        }
+    };
     auto body = [&](int u, int unext) {
         stamp(u, 0);
         // the lane index, opaque per item: the per-thread LDS bases derived from it are then
@@ -685,7 +799,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if constexpr (!(DIAG & 4)) dftw<32, W8>(&v[b * 32]);
         stamp(u, 2);
         if constexpr (STG) {
+            if constexpr (IGS) {  // in-grid state: the previous item's ring stores, drained in every wave
+                if (prev_chunk >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
+            if constexpr (IGS) {
+                if (prev_chunk >= 0) st_signal();
+            }
             stamp(u, 7);
             if constexpr (SPLIT) {  // region B is free until the next item: its half of the next frame now
                 const int fn = frame_of(unext);
@@ -716,6 +836,9 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         }
 
         if (!active) return;
+        if constexpr (IGS) {  // this item's chunk, signalled once its ring stores have drained
+            if (frame >= a.ring_first && igs_on()) prev_chunk = frame / st_args()->st_chunk_len;
+        }
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
         // (kernel B of the large-N pair: kk = s + S*(...) with the runtime S = dif_ss and
         // s = dif_r; the stride and frame length below are then uniform runtime values)
@@ -863,6 +986,20 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     for (int u = u0; u < items; it_count++) {
         const int un = next_item(u);
         body(u, un);
+        if constexpr (IGS) {
+            if (igs_on()) {
+                // between items at most one unit, and only from a complete chunk; after the last
+                // item, drain and signal it, then keep taking units until none is left (one call
+                // site: one inlined copy of the unit code)
+                const bool last = un >= items;
+                if (last && prev_chunk >= 0) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    lds_barrier();
+                    st_signal();
+                }
+                take_units(last ? -1 : 1);
+            }
+        }
         u = un;
     }
 }
@@ -871,7 +1008,9 @@ template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = f
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    const size_t lds = (size_t)G::LDS_BYTES;
+    // + 16 B: the in-grid state's unit broadcast slot (fft_wide_kernel IGS)
+    constexpr bool igs_k = STG && RS == 2 && LOGM == 15 && !CO && (DIAG & ~32) == 0;
+    const size_t lds = (size_t)G::LDS_BYTES + (igs_k ? 16 : 0);
     if (!a.wide_tw) return hipErrorInvalidValue;
     if (RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;

@@ -64,10 +64,10 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
         tr.write_line(f"floor {floor:.0f} dB: {len(xs)} comparisons, {sum(x['bins'] for x in xs)} bins; "
                       f"max |d| live {live['max_live']:.2e} dB (bar {gu.DB_TOL}; {live['test']}); "
                       f"excluded below floor: mean {sum(x['excluded'] for x in xs) / len(xs):.3f}, "
-                      f"max {max(x['excluded'] for x in xs):.3f}; max |d| over every bin both sides resolve (above "
-                      f"the fp32 floor, {gu.RESOLVE_DB:.0f} dB under the row level) {fin['max_finite']:.3e} dB "
+                      f"max {max(x['excluded'] for x in xs):.3f}; max |d| over every bin both sides resolve "
+                      f"(>= 20 dB above fp32 rounding: within {gu.RESOLVE_DB:.0f} dB of the row level) {fin['max_finite']:.3e} dB "
                       f"({fin['test']}); {sum(x['subres'] for x in xs)} bins below that floor on a side "
-                      f"(KAT zeros, fp32 rounding noise) not compared")
+                      f"(KAT zeros, within 20 dB of fp32 rounding noise) not compared")
     for kind, bound in (("every bin (no floor, 0 excluded)", False),
                         ("every bin beyond the reference's own float64 error", True)):
         for bar in sorted({x["bar"] for x in gu.FULL_ROW_LOG if bool(x.get("bound")) == bound}):
