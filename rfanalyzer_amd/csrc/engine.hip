@@ -72,7 +72,7 @@ struct rfa_handle {
     unsigned *d_st_done = nullptr;    // [kStMaxChunks][n >> 10]
     unsigned st_gen = 0;
     bool st_dirty = false;            // counters may be non-zero (a main launch without its state launch)
-    int igs = 1;                      // A/B builds: RFA_IGS=0 off
+    int igs = RFA_IGS;                // in-grid state (A/B builds built with -DRFA_IGS=1; env RFA_IGS=0 off)
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -560,7 +560,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
 #ifdef RFA_AB_BUILD
         if (const char *d = std::getenv("RFA_IGS")) h->igs = std::atoi(d);
 #endif
-        if (logn == 16 && h->d_state_part) {  // in-grid state of the 64 K staged kernels
+        if (RFA_IGS && logn == 16 && h->d_state_part) {  // in-grid state of the 64 K staged kernels
             const size_t done_words = (size_t)rfa::kStMaxChunks * (n / rfa::kStRange);
             if (hipMalloc(&h->d_st_cnt, (rfa::kStMaxChunks + 1) * sizeof(unsigned)) != hipSuccess ||
                 hipMalloc(&h->d_st_done, done_words * sizeof(unsigned)) != hipSuccess)

@@ -125,6 +125,9 @@ struct FftLaunch {
     hipStream_t stream = nullptr;
 };
 constexpr int kStMaxChunks = 32;
+#ifndef RFA_IGS
+#define RFA_IGS 0  // in-grid state compiled in (A/B builds only: a measured loss)
+#endif
 constexpr int kStRange = 1024;  // storage positions per in-grid unit (one per thread of the 32 K workgroup)
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).

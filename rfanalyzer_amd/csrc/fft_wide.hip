@@ -33,6 +33,7 @@ namespace rfa {
 // finished its own items keeps polling for chunks still in flight (s_memrealtime ticks of
 // 10 ns) before it leaves the rest to the finish kernel
 constexpr int kSc1 = 16;
+
 constexpr unsigned long long kStWaitTicks = 4000;
 
 template <int LOGM, int PT>
@@ -609,7 +610,10 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // hand-off forms, row 1).  Nothing ever waits for another workgroup without a bound, so
     // the grid cannot deadlock however many workgroups are resident; units nobody took are
     // computed by state_fused_kernel (fft_kernels.hip), which also folds every summary.
-    constexpr bool IGS = STG && RS == 2 && LOGM == 15 && !COMPLEX_OUT && (DIAG & ~32) == 0;
+    // Measured a loss (profiles/r05/igs_pf_ab.txt: the units' row loads sit behind one round trip
+    // each and the unit code lifts the kernel's SGPR spills 16 -> 74), so it is compiled only
+    // into A/B builds with -DRFA_IGS=1; product builds are the kernel without it.
+    constexpr bool IGS = RFA_IGS && STG && RS == 2 && LOGM == 15 && !COMPLEX_OUT && (DIAG & ~32) == 0;
     // the st_* arguments are read through an opaque kernarg pointer where they are used, so
     // hipcc cannot hoist them into registers held across the FFT (they pushed its SGPR spills
     // 16 -> 104 and cost a VGPR spill when held)
@@ -1008,8 +1012,8 @@ template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = f
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    // + 16 B: the in-grid state's unit broadcast slot (fft_wide_kernel IGS)
-    constexpr bool igs_k = STG && RS == 2 && LOGM == 15 && !CO && (DIAG & ~32) == 0;
+    constexpr bool igs_k = RFA_IGS && STG && RS == 2 && LOGM == 15 && !CO && (DIAG & ~32) == 0;
+    // + 16 B: the in-grid state's unit broadcast slot (IGS, A/B builds with -DRFA_IGS=1)
     const size_t lds = (size_t)G::LDS_BYTES + (igs_k ? 16 : 0);
     if (!a.wide_tw) return hipErrorInvalidValue;
     if (RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table

@@ -249,3 +249,35 @@ def test_config3_batch_every_bin(rfa):
         assert fr <= gu.BATCH_EXCEED_SHARE
         gu.full_row_bound(rows, ref, ref64, bar=gu.DB_TOL_BATCH_EVERY_BIN,
                           label="config 3 batch |librfa - pffft| beyond pffft's error (printed, not asserted)")
+
+
+@pytest.mark.parametrize("seed", gu.CONFIG3_SEEDS)
+def test_config3_no_worse_than_reference(rfa, seed):
+    """BASELINE config 3's batch (500 x 64 K s8 Blackman frames) on four captures: librfa is no
+    worse than the reference's own pffft, both measured against the float64 transform --
+    (1) its share of bins beyond 0.01 dB is at most pffft's, (2) its rounding error on the deep
+    bins (golden_util.deep_bin_error, the error every tail statistic is made of) is at most
+    pffft's, and (3) its worst bin stays within DB_TOL_BATCH_MAX.  The maxima of both and the
+    1e-6 tail quantiles are printed: the maximum over 32.8 M bins is the one deepest bin's
+    rounding draw, so a transform with the smaller error still has the larger maximum on some
+    captures."""
+    if not oracle.ref_available():
+        pytest.skip("reference pffft build (oracle/_ref) absent")
+    n, b = 65536, 500
+    data = signals.frames_bytes(n, b, "s8", seed, tones=((0.1234, 0.4), (-0.377, 0.01)), noise=0.05)
+    with _engine(rfa, n, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(data, b)
+    ref64 = oracle.spectrum_rows(data, oracle.IN_S8, n, b, None, oracle.WIN_BLACKMAN)
+    ref = oracle.ref_spectrum_rows(data, oracle.IN_S8, n, b)
+    sh_l, sh_p = gu.exceed_fraction(rows, ref64), gu.exceed_fraction(ref, ref64)
+    de_l, de_p = gu.deep_bin_error(rows, ref64), gu.deep_bin_error(ref, ref64)
+    mx_l, mx_p = gu.full_row_diff(rows, ref64, bar=None), gu.full_row_diff(ref, ref64, bar=None)
+    q_l, q_p = gu.tail_quantile(rows, ref64), gu.tail_quantile(ref, ref64)
+    raw = gu.full_row_diff(rows, ref, bar=None)
+    gu.NOTES.append(f"config 3 seed {seed:2d} vs float64, librfa / pffft: share > {gu.DB_TOL} dB {sh_l:.2e} / {sh_p:.2e}; "
+                    f"deep-bin error {de_l:.3e} / {de_p:.3e} (ratio {de_l / de_p:.2f}); 1e-6 quantile {q_l:.4f} / "
+                    f"{q_p:.4f} dB; max {mx_l:.4f} / {mx_p:.4f} dB; |librfa - pffft| max {raw:.4f} dB")
+    assert sh_l <= sh_p, (sh_l, sh_p)
+    assert de_l <= de_p, (de_l, de_p)
+    assert mx_l <= gu.DB_TOL_BATCH_MAX
+    gu.assert_same_peak_bins(rows, np.argmax(ref64, 1))
