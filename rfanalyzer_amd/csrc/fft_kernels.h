@@ -117,7 +117,7 @@ struct FftLaunch {
     // fields) folds the summaries, computes the units nobody took, and resets the counters.
     // Never waits: a unit is taken only when its chunk is already complete.
     float4 *st_part = nullptr;
-    unsigned *st_cnt = nullptr;   // [kStMaxChunks] items done per chunk, then the ticket counter
+    unsigned *st_cnt = nullptr;   // [kStCntWords]: items done per chunk, unit tickets per chunk
     unsigned *st_done = nullptr;  // [kStMaxChunks][n >> 10]
     unsigned st_gen = 0;
     int st_chunk_len = 0;  // frames per chunk (<= 32); 0: in-grid state off
@@ -125,10 +125,13 @@ struct FftLaunch {
     hipStream_t stream = nullptr;
 };
 constexpr int kStMaxChunks = 32;
+// st_cnt words: [kStMaxChunks] items done per chunk, [kStMaxChunks] unit tickets per chunk,
+// then kStDbg.. diagnostics (RFA_IGS_DEBUG)
+constexpr int kStDbg = 2 * kStMaxChunks, kStCntWords = kStDbg + 8;
 #ifndef RFA_IGS
 #define RFA_IGS 0  // in-grid state compiled in (A/B builds only: a measured loss)
 #endif
-constexpr int kStRange = 1024;  // storage positions per in-grid unit (one per thread of the 32 K workgroup)
+constexpr int kStRange = 4096;  // storage positions per in-grid unit (four per thread of the 32 K workgroup)
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
 hipError_t launch_fft(const FftLaunch &a);
@@ -195,7 +198,7 @@ struct StateLaunch {
     int max_chunks = 1;
     int fused = 1;           // single-launch chunked scan (RFA_STATE_FUSED=0: partial + combine kernels)
     // in-grid summaries of the main kernel (FftLaunch st_*): chunk c of the 1024-position range
-    // r is read from part[c][pos] when done[c][r] == gen; cnt (kStMaxChunks + 1 words) is reset
+    // r is read from part[c][pos] when done[c][r] == gen; cnt's kStDbg counter words are reset
     const unsigned *done = nullptr;
     unsigned gen = 0;
     unsigned *cnt = nullptr;

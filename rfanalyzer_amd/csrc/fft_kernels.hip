@@ -541,7 +541,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     __shared__ float4 part[CH][BPB];
     const int c = threadIdx.x / TPC, l = threadIdx.x % TPC;
     const int bin = blockIdx.x * BPB + 4 * l;
-    if (a.cnt && blockIdx.x == 0 && threadIdx.x <= kStMaxChunks) a.cnt[threadIdx.x] = 0u;  // in-grid counters
+    if (a.cnt && blockIdx.x == 0 && threadIdx.x < kStDbg) a.cnt[threadIdx.x] = 0u;  // in-grid counters
     // chunk c of this block's bins summarised in-grid by the main kernel (FftLaunch st_*):
     // the same float4 state_step forms, so which kernel formed it does not change the result
     if (a.done && a.done[c * (a.n / kStRange) + blockIdx.x * BPB / kStRange] == a.gen) {

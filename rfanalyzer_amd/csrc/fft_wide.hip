@@ -32,9 +32,15 @@ namespace rfa {
 // the aux operand; the load then bypasses the CU's L1), and how long a workgroup that has
 // finished its own items keeps polling for chunks still in flight (s_memrealtime ticks of
 // 10 ns) before it leaves the rest to the finish kernel
-constexpr int kSc1 = 16;
-
-constexpr unsigned long long kStWaitTicks = 4000;
+[[maybe_unused]] constexpr int kSc1 = 16;
+#ifndef RFA_IGS_WAIT
+#define RFA_IGS_WAIT 0  // 4000 (40 us) cost the kernel +45 us: every workgroup polled for the last chunks
+#endif
+constexpr unsigned long long kStWaitTicks = RFA_IGS_WAIT;
+#ifndef RFA_IGS_TAIL
+#define RFA_IGS_TAIL 1  // units a workgroup may take after its last item (-1: until none is ready;
+                        // the last chunk's units then ran serially on the last workgroups)
+#endif
 
 template <int LOGM, int PT>
 struct WGeo {
@@ -460,6 +466,66 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     }
 }
 
+#if RFA_IGS
+// In-grid state unit (fft_wide_kernel IGS, N = 64 K): chunk c's summary (state_step, the
+// float4 of fft_kernels.hip state_partial_kernel) over kStRange storage positions, four per
+// thread, written to st_part[c][pos].  Row loads are 16-B sc1 loads (the rows were written
+// through by other CUs), 16 frames in flight.  noinline: its registers do not join the FFT
+// body's allocation (inlined, they lifted the kernel's SGPR spills 16 -> 74).
+__device__ __attribute__((noinline)) void st_unit(unsigned karg_lo, unsigned karg_hi, int t_) {
+    using KArg = const __attribute__((address_space(4))) FftLaunch;
+    // (readfirstlane returns int: widen through unsigned, or a low half >= 2^31 sign-extends
+    // over the high half)
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane(karg_lo);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane(karg_hi);
+    KArg *k = (KArg *)(((unsigned long long)hi << 32) | lo);
+    constexpr int n = 1 << 16, ranges = n / kStRange, IF = 16;
+    const int t = __builtin_amdgcn_readfirstlane(t_);
+    const int c = t / ranges, pos = (t - c * ranges) * kStRange + 4 * (int)(threadIdx.x & 1023);
+    const int cl = k->st_chunk_len, f0 = c * cl, nf = min(k->n_frames - f0, cl);
+    const int rows = k->ring_rows;
+    int rr = (k->ring_base - f0) % rows;
+    if (rr < 0) rr += rows;
+    const rsrc_t rs = make_rsrc(k->ring, (unsigned)rows * (unsigned)(n * 4));
+    const unsigned base = (unsigned)pos * 4u, rowb = (unsigned)n * 4u;
+    // row of frame f0 + j: rr - j, wrapping below 0 (FftProcessor.kt:226-227 writeIndex--)
+    // (frames past the chunk: an offset past num_records, which reads zeros without a memory
+    // access -- the loads stay unconditional, so the compiler counts them with vmcnt(N) instead
+    // of draining at every branch: conditional loads cost 50 vmcnt(0) waits, ~30 us a unit)
+    auto voff = [&](int j) {
+        return j < nf ? (int)(base + (unsigned)(j <= rr ? rr - j : rr - j + rows) * rowb) : (int)0x80000000u;
+    };
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    f4v x[IF];
+#pragma unroll
+    for (int j = 0; j < IF; j++) x[j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff(j), 0, kSc1));
+    float pk[4], emi[4], b[4];
+    bool restart[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) pk[q] = emi[q] = -INFINITY, b[q] = 0.0f, restart[q] = false;
+    float am = 1.0f;
+    const float al = k->st_alpha, keep = 1.0f - al;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        const f4v v = x[j % IF];
+        if (j + IF < 32)  // refill the slot: IF frames stay in flight
+            x[j % IF] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff(j + IF), 0, kSc1));
+        if (j < nf) {
+            state_step(pk[0], emi[0], b[0], restart[0], v.x, al);
+            state_step(pk[1], emi[1], b[1], restart[1], v.y, al);
+            state_step(pk[2], emi[2], b[2], restart[2], v.z, al);
+            state_step(pk[3], emi[3], b[3], restart[3], v.w, al);
+            am *= keep;
+        }
+    }
+    const rsrc_t ps = make_rsrc(k->st_part + (size_t)c * n, n * 16);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+        buf_store_f32x4(pk[q], restart[q] ? -1.0f : am, b[q], emi[q], ps, (pos + q) * 16, 0);
+    if ((threadIdx.x & 1023) == 0) k->st_done[t] = k->st_gen;
+}
+#endif
+
 // DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
 // 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
 // STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
@@ -610,9 +676,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // hand-off forms, row 1).  Nothing ever waits for another workgroup without a bound, so
     // the grid cannot deadlock however many workgroups are resident; units nobody took are
     // computed by state_fused_kernel (fft_kernels.hip), which also folds every summary.
-    // Measured a loss (profiles/r05/igs_pf_ab.txt: the units' row loads sit behind one round trip
-    // each and the unit code lifts the kernel's SGPR spills 16 -> 74), so it is compiled only
-    // into A/B builds with -DRFA_IGS=1; product builds are the kernel without it.
+    // Compiled only into builds with -DRFA_IGS=1 (round-5 A/B: profiles/r05/igs_*).
     constexpr bool IGS = RFA_IGS && STG && RS == 2 && LOGM == 15 && !COMPLEX_OUT && (DIAG & ~32) == 0;
     // the st_* arguments are read through an opaque kernarg pointer where they are used, so
     // hipcc cannot hoist them into registers held across the FFT (they pushed its SGPR spills
@@ -636,78 +700,81 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         return k->st_chunk_len > 0 && k->ring != nullptr && k->rows == nullptr;
     };
     int prev_chunk = -1;  // chunk of the previous item while its completion is not yet signalled
+#ifdef RFA_IGS_DEBUG
+    if constexpr (IGS) {
+        if (threadIdx.x == 0 && a.st_cnt) {
+            __hip_atomic_fetch_add(&a.st_cnt[kStDbg + 6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (igs_on()) __hip_atomic_fetch_add(&a.st_cnt[kStDbg + 7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+#endif
     auto st_signal = [&] {  // after every wave's vmcnt(0) and a barrier
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             __hip_atomic_fetch_add(&st_args()->st_cnt[prev_chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef RFA_IGS_DEBUG
+            __hip_atomic_fetch_add(&st_args()->st_cnt[kStDbg + 2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        }
         prev_chunk = -1;
     };
     auto run_unit = [&](int t) {
-        KArg *k = st_args();
-        constexpr int ranges = M * RS / kStRange;
-        const int c = t / ranges, pos = (t - c * ranges) * kStRange + (int)threadIdx.x;
-        const int cl = k->st_chunk_len, f0 = c * cl, nf = min(k->n_frames - f0, cl);
-        const int rows = k->ring_rows;
-        int rr = (k->ring_base - f0) % rows;
-        if (rr < 0) rr += rows;
-        const rsrc_t rs = make_rsrc(k->ring, (unsigned)rows * (unsigned)(n * 4));
-        // the row offset rides in the lane offset, one register stepped per frame: 32 uniform
-        // row offsets held at once would raise the kernel's SGPR pressure (and spill the FFT's)
-        unsigned voff = (unsigned)rr * (unsigned)(n * 4) + (unsigned)pos * 4u;
-        const unsigned wrap = (unsigned)rows * (unsigned)(n * 4);
-        float x[32];
-#pragma unroll
-        for (int j = 0; j < 32; j++) {  // every frame of the chunk in flight (sc1: written through by other CUs)
-            if (j < nf) x[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, 0, kSc1));
-            voff = rr == 0 ? voff + wrap - n * 4 : voff - n * 4;  // FftProcessor.kt:226-227: frame f + 1 one row earlier
-            rr = rr == 0 ? rows - 1 : rr - 1;
-        }
-        float pk = -INFINITY, emi = -INFINITY, b = 0.0f, am = 1.0f;
-        bool restart = false;
-        const float al = k->st_alpha, keep = 1.0f - al;
-#pragma unroll
-        for (int j = 0; j < 32; j++) {
-            if (j < nf) {
-                state_step(pk, emi, b, restart, x[j], al);
-                am *= keep;
-            }
-        }
-        buf_store_f32x4(pk, restart ? -1.0f : am, b, emi, make_rsrc(k->st_part + (size_t)c * n, n * 16), pos * 16, 0);
-        if (threadIdx.x == 0) k->st_done[t] = k->st_gen;
+#if RFA_IGS
+        const unsigned long long kp = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
+        st_unit((unsigned)kp, (unsigned)(kp >> 32), t);
+#endif
+        (void)t;
         pending_st = 0;  // the unit waited for its loads, so everything older (the staged frame) landed too
     };
+    // thread 0's first chunk not known to be exhausted (its tickets all taken)
+    int st_floor = 0;
     auto take_units = [&](int max_units) {
         constexpr int ranges = M * RS / kStRange;
         int *lds_slot = reinterpret_cast<int *>(lds + G::TW_LDS + G::SLOTS * G::HALFP);
         for (int it = 0; max_units < 0 || it < max_units; it++) {
             if (threadIdx.x == 0) {
                 KArg *k = st_args();
-                const int cl = k->st_chunk_len, nfr = k->n_frames;
-                const int total = ((nfr + cl - 1) / cl) * ranges;
+                const int cl = k->st_chunk_len, nfr = k->n_frames, nch = (nfr + cl - 1) / cl;
                 unsigned *cnt = k->st_cnt, *tickets = cnt + kStMaxChunks;
-                auto ready = [&](unsigned t) {
-                    const int c = (int)t / ranges;
-                    const unsigned need = 2u * (unsigned)min(nfr - c * cl, cl);  // RS = 2 items per frame
-                    return __hip_atomic_load(&cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= need;
-                };
                 const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + kStWaitTicks;
-                int unit = -1;  // -1: none (stop), >= 0: run it, -2: a ticket the finish kernel will serve
+                int unit = -1;  // -1: none (stop), >= 0: run it
+                // per-chunk tickets: a fetch-add on chunk c's counter either returns one of its
+                // units or says the chunk is exhausted -- no unit is lost and nobody retries.
+                // (One shared ticket lost ~150 of 256 units a call to a stale ready check; a
+                // compare-exchange on it serialised the grid on its retries: 8000 per call, 520 us.)
                 for (;;) {
-                    const unsigned t = __hip_atomic_load(tickets, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((int)t >= total) break;
-                    if (ready(t)) {
-                        const unsigned mine = __hip_atomic_fetch_add(tickets, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if ((int)mine < total) unit = ready(mine) ? (int)mine : -2;
-                        break;
+                    bool pending = false;
+                    for (int c = st_floor; c < nch; c++) {
+                        if (__hip_atomic_load(&tickets[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)ranges) {
+                            st_floor = c + 1;
+                            continue;
+                        }
+                        const unsigned need = 2u * (unsigned)min(nfr - c * cl, cl);  // RS = 2 items per frame
+                        if (__hip_atomic_load(&cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                            pending = true;  // chunks complete about in order: stop at the first open one
+                            break;
+                        }
+                        const unsigned m = __hip_atomic_fetch_add(&tickets[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (m < (unsigned)ranges) {
+                            unit = c * ranges + (int)m;
+                            break;
+                        }
+                        st_floor = c + 1;
+#ifdef RFA_IGS_DEBUG
+                        __hip_atomic_fetch_add(&cnt[kStDbg + 4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                     }
-                    if (max_units >= 0 || __builtin_amdgcn_s_memrealtime() >= t_end) break;
+                    if (unit >= 0 || !pending || max_units >= 0 || __builtin_amdgcn_s_memrealtime() >= t_end) break;
                     __builtin_amdgcn_s_sleep(16);
                 }
+#ifdef RFA_IGS_DEBUG
+                __hip_atomic_fetch_add(&cnt[kStDbg + (unit >= 0 ? 3 : 5)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
                 lds_slot[it & 1] = unit;
             }
             lds_barrier();
             const int unit = __builtin_amdgcn_readfirstlane(lds_slot[it & 1]);  // uniform: descriptors in SGPRs
             if (unit == -1) break;
-            if (unit >= 0) run_unit(unit);
+            run_unit(unit);
         }
     };
     auto body = [&](int u, int unext) {
@@ -1001,7 +1068,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                     lds_barrier();
                     st_signal();
                 }
-                take_units(last ? -1 : 1);
+                take_units(last ? RFA_IGS_TAIL : 1);
             }
         }
         u = un;

@@ -613,11 +613,8 @@ hipError_t launch64_x(const FftLaunch &a) {
 // kernel for every format, so it is compiled into A/B builds only (all formats, or the
 // RFA_W64_FORMATS environment mask).
 #ifndef RFA_W64_FORMATS
-#ifdef RFA_AB_BUILD
-#define RFA_W64_FORMATS 0x1f
-#else
-#define RFA_W64_FORMATS 0
-#endif
+#define RFA_W64_FORMATS 0  // A/B builds too: N = 64 K takes the product's wide kernel unless the
+                           // RFA_W64_FORMATS environment mask selects this one
 #endif
 bool w64_format(int fmt) {
 #ifdef RFA_AB_BUILD
