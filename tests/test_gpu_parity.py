@@ -257,10 +257,12 @@ def test_config3_no_worse_than_reference(rfa, seed):
     worse than the reference's own pffft, both measured against the float64 transform --
     (1) its share of bins beyond 0.01 dB is at most pffft's, (2) its rounding error on the deep
     bins (golden_util.deep_bin_error, the error every tail statistic is made of) is at most
-    pffft's, and (3) its worst bin stays within DB_TOL_BATCH_MAX.  The maxima of both and the
-    1e-6 tail quantiles are printed: the maximum over 32.8 M bins is the one deepest bin's
-    rounding draw, so a transform with the smaller error still has the larger maximum on some
-    captures."""
+    pffft's, (3) its 1e-6 tail quantile (golden_util.tail_quantile) is at most pffft's, and
+    (4) its worst bin stays within DB_TOL_BATCH_MAX.  The maxima of both are printed, not
+    compared: the maximum over 32.8 M bins is one deep bin's rounding draw, so a transform with
+    the smaller error still has the larger maximum on some captures -- computing one more stage
+    exactly moves seed 11's maximum from 0.088 to 0.120 dB (profiles/r05/
+    precision_seed11_stage_sweep.txt)."""
     if not oracle.ref_available():
         pytest.skip("reference pffft build (oracle/_ref) absent")
     n, b = 65536, 500
@@ -279,5 +281,6 @@ def test_config3_no_worse_than_reference(rfa, seed):
                     f"{q_p:.4f} dB; max {mx_l:.4f} / {mx_p:.4f} dB; |librfa - pffft| max {raw:.4f} dB")
     assert sh_l <= sh_p, (sh_l, sh_p)
     assert de_l <= de_p, (de_l, de_p)
+    assert q_l <= q_p, (q_l, q_p)  # the tail: the 33 worst bins of 32.8 M, no worse than pffft's
     assert mx_l <= gu.DB_TOL_BATCH_MAX
     gu.assert_same_peak_bins(rows, np.argmax(ref64, 1))
