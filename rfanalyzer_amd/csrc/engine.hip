@@ -39,6 +39,9 @@ struct rfa_handle {
     float2 *d_w64_tw = nullptr;       // N = 64 K: the wave-decoupled kernel's twiddle blob (fft_w64.hip)
     // N = 2^18..2^20 (decimation in frequency, fft_large.hip)
     float2 *d_dit_c = nullptr, *d_dit_d = nullptr;  // W_N^{m s} = C[s][m >> 7] * D[s][m & 127]
+    float2 *d_dit_cp = nullptr, *d_dit_dp = nullptr;  // the pipelined 8-bit kernel's split (rfa::dif_lo_points)
+    uint8_t *d_dit_in = nullptr;      // misaligned 8-bit frames, copied 16-B aligned for the pipelined kernel
+    size_t d_dit_in_cap = 0;
     float2 *d_dit_y = nullptr;        // scratch z [frames][S][M] complex
     size_t d_dit_y_cap = 0;
     float *d_dit_db = nullptr;        // caller rows of a batch, residue-major, before cols_to_rows
@@ -246,6 +249,20 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         A.window = a.window;  // natural order: the scaled window or a seam window
         A.tw_c = h->d_dit_c;
         A.tw_d = h->d_dit_d;
+        A.tw_cp = h->d_dit_cp;
+        A.tw_dp = h->d_dit_dp;
+        if (A.pipe > 0 && A.fmt <= 1 && ((reinterpret_cast<uintptr_t>(A.in) | (uintptr_t)A.frame_stride) & 15) != 0) {
+            // misaligned 8-bit frames: an aligned copy, so every 8-bit frame takes the same kernel
+            // (and the same rounding) whatever the caller's pointer
+            const size_t fb = (size_t)n * 2;
+            if (ensure_device_buffer(h, (void **)&h->d_dit_in, &h->d_dit_in_cap, (size_t)h->dit_frames * fb))
+                return hipErrorOutOfMemory;
+            hipError_t e = hipMemcpy2DAsync(h->d_dit_in, fb, A.in, (size_t)A.frame_stride, fb, cnt, hipMemcpyDeviceToDevice,
+                                            a.stream);
+            if (e != hipSuccess) return e;
+            A.in = h->d_dit_in;
+            A.frame_stride = (long long)fb;
+        }
         A.z = h->d_dit_y;
         A.pipe = h->dif_pipe;
         A.stream = a.stream;
@@ -480,11 +497,14 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         }
     }
     if (logn > 17) {  // decimation in frequency: S column DFTs, then S sub-FFTs of M = 32768 points
-        std::vector<float2> c, d, blob = rfa::wide_twiddles(rfa::kDitLogM, rfa::kWidePT, rfa::kDitLogM);
-        rfa::dif_twiddles(logn, c, d);
+        std::vector<float2> c, d, cp, dp, blob = rfa::wide_twiddles(rfa::kDitLogM, rfa::kWidePT, rfa::kDitLogM);
+        rfa::dif_twiddles(logn, rfa::dif_lo_points(false), c, d);
+        rfa::dif_twiddles(logn, rfa::dif_lo_points(true), cp, dp);
         struct { void **dst; const void *src; size_t bytes; } up[] = {
             {(void **)&h->d_dit_c, c.data(), c.size() * sizeof(float2)},
             {(void **)&h->d_dit_d, d.data(), d.size() * sizeof(float2)},
+            {(void **)&h->d_dit_cp, cp.data(), cp.size() * sizeof(float2)},
+            {(void **)&h->d_dit_dp, dp.data(), dp.size() * sizeof(float2)},
             {(void **)&h->d_wide_tw, blob.data(), blob.size() * sizeof(float2)}};
         for (auto &u : up) {
             if (hipMalloc(u.dst, u.bytes) != hipSuccess) return bail(RFA_ERR_NOMEM);
@@ -594,6 +614,9 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_w64_tw);
     hipFree(h->d_dit_c);
     hipFree(h->d_dit_d);
+    hipFree(h->d_dit_cp);
+    hipFree(h->d_dit_dp);
+    hipFree(h->d_dit_in);
     hipFree(h->d_dit_y);
     hipFree(h->d_dit_db);
     hipFree(h->d_twc);

@@ -562,6 +562,12 @@ __device__ __forceinline__ void buf_store_f32x4(float a, float b, float c, float
     (void)v; (void)rs; (void)voff; (void)soff;
 #endif
 }
+// the same 16-B store without sc1 (write-back in the XCD's L2)
+__device__ __forceinline__ void buf_store_f32x4_wb(float a, float b, float c, float d, rsrc_t rs, int voff, int soff) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) int, (f32x4){a, b, c, d}),
+                                           rs, voff, soff, 0);
+}
 __device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, int soff) {
     typedef int i32x2 __attribute__((ext_vector_type(2)));
     i32x2 v = {__builtin_bit_cast(int, x.x), __builtin_bit_cast(int, x.y)};

@@ -166,10 +166,13 @@ struct DifLaunch {
     int fmt = 0;
     int logn = 0;
     const float *window = nullptr;  // natural order, N floats (scaled or seam window)
-    const float2 *tw_c = nullptr;   // [S][M/128]  W_N^{s * 128 * mhi}
+    const float2 *tw_c = nullptr;   // [S][M/128]  W_N^{s * 128 * mhi}  (per-tile kernel)
     const float2 *tw_d = nullptr;   // [S][128]    W_N^{s * mlo} - 1
+    const float2 *tw_cp = nullptr;  // the pipelined kernel's split: [S][M/LO], [S][LO] (dif_lo_points(true))
+    const float2 *tw_dp = nullptr;
     float2 *z = nullptr;            // scratch [n_frames][S][M]
-    int pipe = 6;                   // 8-bit, 16-B aligned frames: pipelined kernel with `pipe` frame groups (0: off)
+    int pipe = 6;                   // 8-bit, 16-B aligned frames: pipelined kernel with `pipe` frame groups (0: off;
+                                    // the engine stages misaligned 8-bit frames to an aligned copy for it)
     hipStream_t stream = nullptr;
 };
 constexpr int kDitLogM = 15;
@@ -178,7 +181,9 @@ constexpr int kFmtDif = 5;  // wide-kernel input: kernel A's scratch (complex f3
 hipError_t launch_dif_front(const DifLaunch &a);
 // kernel B's residue-major dB rows -> natural order (caller rows of the large-N pair)
 hipError_t launch_cols_to_rows(const float *cols, float *rows, int n_frames, int logn, hipStream_t st);
-void dif_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d);
+// points of the twiddle split's fine table: the pipelined 8-bit kernel's (pipe) or the per-tile kernel's
+int dif_lo_points(bool pipe);
+void dif_twiddles(int logn, int lo, std::vector<float2> &c, std::vector<float2> &d);
 
 // Sequential EMA / peak-hold over n_frames rows.  Row f is at
 // rows + f*row_stride, or, when ring_rows > 0, at rows + ((ring_base - f) mod ring_rows)*n

@@ -32,10 +32,16 @@
 
 namespace rfa {
 
+// Twiddle split m = khi * 2^LO + klo of W_N^{m s} = C[s][khi] (1 + D[s][klo]) (khi is wave-uniform
+// for LO >= 6).  The per-tile kernel (16/32-bit input) keeps LO = 7; the pipelined 8-bit kernel
+// takes LO = 6: its D table halves to 16 KB of LDS (round 5, profiles/r05/large_n_front_ab.txt).
 #ifndef RFA_DIF_LOBITS
-#define RFA_DIF_LOBITS 7  // twiddle split m = khi * 2^LOBITS + klo (khi wave-uniform while LOBITS >= 6)
+#define RFA_DIF_LOBITS 6  // the pipelined kernel's LO (A/B: 7)
 #endif
-constexpr int kDifLo = 1 << RFA_DIF_LOBITS;
+constexpr int kDifLoTile = 128, kDifLoPipe = 1 << RFA_DIF_LOBITS;
+#ifndef RFA_DIF_SC1
+#define RFA_DIF_SC1 1  // z stores write-through (sc1): the scratch leaves the XCD's L2 for kernel B
+#endif
 
 template <int S, int FMT>
 __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
@@ -100,8 +106,8 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     dft<S>(v);  // v[s] = sum_j x w W_S^{j s}
     // m >> 7 is the same for the 64 lanes of a wave (256-thread blocks of consecutive m):
     // the C factors are scalar loads
-    const int khi = __builtin_amdgcn_readfirstlane(m >> RFA_DIF_LOBITS), klo = m & (kDifLo - 1);
-    constexpr int mc = M >> RFA_DIF_LOBITS;
+    const int khi = __builtin_amdgcn_readfirstlane(m >> 7), klo = m & (kDifLoTile - 1);
+    constexpr int mc = M / kDifLoTile;
     // W_N^{m s} = C (1 + delta): the small correction C * delta is added last, so the
     // twiddle carries C's rounding and one add instead of a full product's.  Chunks
     // of 8 (scheduling barriers) keep the delta loads from all being live at once.
@@ -109,7 +115,7 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
     for (int s0 = 0; s0 < S; s0 += 8) {
         float2 d[8];
 #pragma unroll
-        for (int s = s0; s < s0 + 8 && s < S; s++) d[s - s0] = a.tw_d[s * kDifLo + klo];
+        for (int s = s0; s < s0 + 8 && s < S; s++) d[s - s0] = a.tw_d[s * kDifLoTile + klo];
 #pragma unroll
         for (int s = (s0 ? s0 : 1); s < s0 + 8 && s < S; s++) {
             const float2 c = a.tw_c[s * mc + khi], corr = cmul(c, d[s - s0]);
@@ -138,12 +144,12 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
 #define RFA_DIF_DGLOBAL 0  // D factors read through L1 instead of the 32 KB LDS table
 #endif
 #ifndef RFA_DIF_ST16
-#define RFA_DIF_ST16 0  // z stored 16 B per lane: lane pairs swap one value per two rows
+#define RFA_DIF_ST16 1  // z stored 16 B per lane: lane pairs swap one value per two rows (A/B: 0)
 #endif
 template <int S, int FMT, int BW = 256>
 __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pipe_kernel(DifLaunch a, int groups) {
     static_assert(FMT <= 1, "8-bit formats");
-    constexpr int M = 1 << kDitLogM, n = S * M, mc = M >> RFA_DIF_LOBITS;
+    constexpr int M = 1 << kDitLogM, n = S * M, mc = M / kDifLoPipe;
     constexpr int SB = 2, NW = BW / 64;
     constexpr int ROWB = BW * SB, TILEB = S * ROWB, NPIECE = TILEB / 1024, PPW = NPIECE / NW;
     constexpr int RPP = ROWB >= 1024 ? 1 : 1024 / ROWB, LPR = 64 / RPP;  // tile rows per 1 KiB piece, lanes per row
@@ -151,9 +157,9 @@ __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pip
     static_assert(NPIECE % NW == 0 && RPP >= 1, "whole pieces per wave");
     __shared__ __attribute__((aligned(16))) uint8_t tile[TILEB];
 #if RFA_DIF_DGLOBAL
-    const float2 *dtab = a.tw_d;
+    const float2 *dtab = a.tw_dp;
 #else
-    __shared__ float2 dtab[S * kDifLo];
+    __shared__ float2 dtab[S * kDifLoPipe];
 #endif
     const int bx = blockIdx.x % (M / BW), g0 = blockIdx.x / (M / BW);
     const int m0 = bx * BW, m = m0 + threadIdx.x;
@@ -175,23 +181,23 @@ __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pip
         }
     };
 #if !RFA_DIF_DGLOBAL
-    for (int e = threadIdx.x; e < S * kDifLo; e += BW) dtab[e] = a.tw_d[e];
+    for (int e = threadIdx.x; e < S * kDifLoPipe; e += BW) dtab[e] = a.tw_dp[e];
 #endif
     const rsrc_t w_rs = make_rsrc(a.window, n * 4);
     float w[S];
 #pragma unroll
     for (int j = 0; j < S; j++) w[j] = buf_load_f32(w_rs, m * 4, j * M * 4);
-    const int khi = __builtin_amdgcn_readfirstlane(m >> RFA_DIF_LOBITS), klo = m & (kDifLo - 1);
+    const int khi = __builtin_amdgcn_readfirstlane(m >> RFA_DIF_LOBITS), klo = m & (kDifLoPipe - 1);
     // C factors through the constant address space: the index is wave-uniform, so they
     // are scalar loads (s_load_dwordx2) instead of a uniform-address VMEM load per s
-    const auto *tw_c_s = (const __attribute__((address_space(4))) f2v *)(uintptr_t)a.tw_c;
+    const auto *tw_c_s = (const __attribute__((address_space(4))) f2v *)(uintptr_t)a.tw_cp;
     auto c_at = [&](int i) { return from_v(tw_c_s[i]); };
     if (g0 < a.n_frames) stage(g0);
     bool first = true;
     for (int f = g0; f < a.n_frames; f += groups) {
-        // this frame's tile has landed (younger than its DMA: the previous frame's S stores)
+        // this frame's tile has landed (younger than its DMA: the previous frame's z stores, S or S / 2)
         if (first) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(S) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(RFA_DIF_ST16 ? S / 2 : S) : "memory");
         first = false;
         float2 v[S];
 #pragma unroll
@@ -206,27 +212,32 @@ __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pip
         {  // W_N^{m s} = C (1 + delta), as dif_front_kernel; C in SGPRs (scalar loads,
            // profiles/r03/dif_front_smem_ab.txt)
             {
-                const float2 c = c_at(mc + khi), corr = cmul(c, dtab[kDifLo + klo]);
+                const float2 c = c_at(mc + khi), corr = cmul(c, dtab[kDifLoPipe + klo]);
                 v[1] = cmul(v[1], make_float2(c.x + corr.x, c.y + corr.y));
             }
 #pragma unroll
             for (int s = 2; s < S; s += 2)
-                twiddle_cd2(v[s], dtab[s * kDifLo + klo], c_at(s * mc + khi), v[s + 1], dtab[(s + 1) * kDifLo + klo],
+                twiddle_cd2(v[s], dtab[s * kDifLoPipe + klo], c_at(s * mc + khi), v[s + 1], dtab[(s + 1) * kDifLoPipe + klo],
                             c_at((s + 1) * mc + khi));
         }
         const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
 #if RFA_DIF_ST16
         // rows s, s + 1 of the column pair (m & ~1, m | 1): the even lane stores row s, the odd
-        // lane row s + 1, each 16 B (both columns); each gives its partner the value it lacks
-        const int p = lane & 1;
+        // lane row s + 1, each 16 B (both columns).  Both rows' values cross (DPP quad_perm
+        // 1,0,3,2) and each lane picks: a select between v[s] and v[s + 1] themselves would become
+        // a select of addresses and put v[] on the stack (S = 16: 80 B of scratch, +35 %)
+        const bool p = (lane & 1) != 0;
+        auto swap = [](float2 x) {
+            return make_float2(
+                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.x), 0xB1, 0xF, 0xF, false)),
+                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.y), 0xB1, 0xF, 0xF, false)));
+        };
 #pragma unroll
         for (int s = 0; s < S; s += 2) {
-            const float2 send = p ? v[s] : v[s + 1];
-            const float2 recv = make_float2(
-                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send.x), 0xB1, 0xF, 0xF, false)),
-                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send.y), 0xB1, 0xF, 0xF, false)));
-            const float2 lo = p ? recv : v[s], hi = p ? v[s + 1] : recv;
-            buf_store_f32x4(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
+            const float2 r0 = swap(v[s]), r1 = swap(v[s + 1]);  // the partner's rows s, s + 1
+            const float2 lo = p ? r1 : v[s], hi = p ? v[s + 1] : r0;
+            if constexpr (RFA_DIF_SC1) buf_store_f32x4(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
+            else buf_store_f32x4_wb(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
         }
 #else
 #pragma unroll
@@ -293,20 +304,22 @@ hipError_t launch_cols_to_rows(const float *cols, float *rows, int n_frames, int
     return hipGetLastError();
 }
 
-void dif_twiddles(int logn, std::vector<float2> &c, std::vector<float2> &d) {
-    const int m = 1 << kDitLogM, s = 1 << (logn - kDitLogM), mc = m >> RFA_DIF_LOBITS;
+int dif_lo_points(bool pipe) { return pipe ? kDifLoPipe : kDifLoTile; }
+
+void dif_twiddles(int logn, int lo, std::vector<float2> &c, std::vector<float2> &d) {
+    const int m = 1 << kDitLogM, s = 1 << (logn - kDitLogM), mc = m / lo;
     const double n = (double)(1 << logn);
     auto w = [&](double e) {  // exp(-2 pi i e / N), correctly rounded from double
         const double ang = -2.0 * M_PI * e / n;
         return make_float2((float)std::cos(ang), (float)std::sin(ang));
     };
     c.assign((size_t)s * mc, make_float2(1.f, 0.f));
-    d.assign((size_t)s * kDifLo, make_float2(1.f, 0.f));
+    d.assign((size_t)s * lo, make_float2(1.f, 0.f));
     for (int r = 0; r < s; r++) {
-        for (int h = 0; h < mc; h++) c[(size_t)r * mc + h] = w(std::fmod((double)r * (double)kDifLo * h, n));
-        for (int l = 0; l < kDifLo; l++) {  // delta = W_N^{r l} - 1: (-2 sin^2(a/2), sin a) from double
+        for (int h = 0; h < mc; h++) c[(size_t)r * mc + h] = w(std::fmod((double)r * (double)lo * h, n));
+        for (int l = 0; l < lo; l++) {  // delta = W_N^{r l} - 1: (-2 sin^2(a/2), sin a) from double
             const double ang = -2.0 * M_PI * (double)r * l / n, h = std::sin(0.5 * ang);
-            d[(size_t)r * kDifLo + l] = make_float2((float)(-2.0 * h * h), (float)std::sin(ang));
+            d[(size_t)r * lo + l] = make_float2((float)(-2.0 * h * h), (float)std::sin(ang));
         }
     }
 }
