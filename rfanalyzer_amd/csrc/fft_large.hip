@@ -42,6 +42,43 @@ constexpr int kDifLoTile = 128, kDifLoPipe = 1 << RFA_DIF_LOBITS;
 #ifndef RFA_DIF_SC1
 #define RFA_DIF_SC1 1  // z stores write-through (sc1): the scratch leaves the XCD's L2 for kernel B
 #endif
+#ifndef RFA_DIF_WPE
+#define RFA_DIF_WPE 1  // minimum waves per SIMD the compiler must allow (4: <= 128 VGPRs)
+#endif
+#ifndef RFA_DIF_DGLOBAL
+#define RFA_DIF_DGLOBAL 0  // D factors read through L1 instead of the 32 KB LDS table
+#endif
+#ifndef RFA_DIF_ST16
+#define RFA_DIF_ST16 1  // z stored 16 B per lane: lane pairs swap one value per two rows (A/B: 0)
+#endif
+
+// The S rows of column m into z (row s at s * M): 16 B per lane (RFA_DIF_ST16) -- rows s, s + 1 of
+// the column pair (m & ~1, m | 1): the even lane stores row s, the odd lane row s + 1, each both
+// columns.  Both rows' values cross (DPP quad_perm 1,0,3,2) and each lane picks: a select between
+// v[s] and v[s + 1] themselves became a select of addresses and put v[] on the stack (S = 16: 80 B
+// of scratch, +35 %).  Write-through (sc1): kernel B reads z from other XCDs.
+template <int S>
+__device__ __forceinline__ void store_z(const float2 *v, rsrc_t z_rs, int m) {
+    constexpr int M = 1 << kDitLogM;
+#if RFA_DIF_ST16
+    const bool p = (m & 1) != 0;
+    auto swap = [](float2 x) {
+        return make_float2(
+            __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.x), 0xB1, 0xF, 0xF, false)),
+            __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.y), 0xB1, 0xF, 0xF, false)));
+    };
+#pragma unroll
+    for (int s = 0; s < S; s += 2) {
+        const float2 r0 = swap(v[s]), r1 = swap(v[s + 1]);  // the partner's rows s, s + 1
+        const float2 lo = p ? r1 : v[s], hi = p ? v[s + 1] : r0;
+        if constexpr (RFA_DIF_SC1) buf_store_f32x4(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
+        else buf_store_f32x4_wb(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
+    }
+#else
+#pragma unroll
+    for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
+#endif
+}
 
 template <int S, int FMT>
 __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
@@ -123,9 +160,7 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
         }
         __builtin_amdgcn_sched_barrier(0);
     }
-    const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
-#pragma unroll
-    for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
+    store_z<S>(v, make_rsrc(a.z + (size_t)f * n, n * 8), m);
 }
 
 // 8-bit formats, persistent and pipelined: block b owns the 256 columns
@@ -137,15 +172,6 @@ __global__ void __launch_bounds__(256) dif_front_kernel(DifLaunch a) {
 // overlap instead of every block loading, then storing, in lock step.
 // BW columns per block.  512-column blocks (one D table per 8 waves, 4 waves per SIMD) measured
 // -1.4 % at 1 M with the ring and +3 % at 256 K / 512 K (profiles/r04/dif_block_width_ab.txt)
-#ifndef RFA_DIF_WPE
-#define RFA_DIF_WPE 1  // minimum waves per SIMD the compiler must allow (4: <= 128 VGPRs)
-#endif
-#ifndef RFA_DIF_DGLOBAL
-#define RFA_DIF_DGLOBAL 0  // D factors read through L1 instead of the 32 KB LDS table
-#endif
-#ifndef RFA_DIF_ST16
-#define RFA_DIF_ST16 1  // z stored 16 B per lane: lane pairs swap one value per two rows (A/B: 0)
-#endif
 template <int S, int FMT, int BW = 256>
 __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pipe_kernel(DifLaunch a, int groups) {
     static_assert(FMT <= 1, "8-bit formats");
@@ -221,28 +247,7 @@ __global__ void __launch_bounds__(BW, BW >= 512 ? 2 : RFA_DIF_WPE) dif_front_pip
                             c_at((s + 1) * mc + khi));
         }
         const rsrc_t z_rs = make_rsrc(a.z + (size_t)f * n, n * 8);
-#if RFA_DIF_ST16
-        // rows s, s + 1 of the column pair (m & ~1, m | 1): the even lane stores row s, the odd
-        // lane row s + 1, each 16 B (both columns).  Both rows' values cross (DPP quad_perm
-        // 1,0,3,2) and each lane picks: a select between v[s] and v[s + 1] themselves would become
-        // a select of addresses and put v[] on the stack (S = 16: 80 B of scratch, +35 %)
-        const bool p = (lane & 1) != 0;
-        auto swap = [](float2 x) {
-            return make_float2(
-                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.x), 0xB1, 0xF, 0xF, false)),
-                __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x.y), 0xB1, 0xF, 0xF, false)));
-        };
-#pragma unroll
-        for (int s = 0; s < S; s += 2) {
-            const float2 r0 = swap(v[s]), r1 = swap(v[s + 1]);  // the partner's rows s, s + 1
-            const float2 lo = p ? r1 : v[s], hi = p ? v[s + 1] : r0;
-            if constexpr (RFA_DIF_SC1) buf_store_f32x4(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
-            else buf_store_f32x4_wb(lo.x, lo.y, hi.x, hi.y, z_rs, ((m - p) + p * M) * 8, s * M * 8);
-        }
-#else
-#pragma unroll
-        for (int s = 0; s < S; s++) buf_store_f32x2(v[s], z_rs, m * 8, s * M * 8);
-#endif
+        store_z<S>(v, z_rs, m);
     }
 }
 
