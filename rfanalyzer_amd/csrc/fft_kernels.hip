@@ -100,6 +100,19 @@ __device__ __forceinline__ void lds_write(const float2 (&v)[16], float2 *buf, in
     }
 }
 
+#ifndef RFA_ROWS_WAVESYNC
+#define RFA_ROWS_WAVESYNC 1
+#endif
+// The exchange of a sub-FFT of <= 64 threads stays inside one wave (its slot's LDS region is its
+// own): a wave's DS instructions execute in order, so its writes are visible to its later reads
+// and its reads precede its later writes -- a compiler fence and the lgkmcnt wait replace the
+// workgroup barrier, and the workgroup's waves run their passes independently.
+template <int LOGM>
+__device__ __forceinline__ void exchange_sync() {
+    if constexpr (RFA_ROWS_WAVESYNC && Geo<LOGM>::TPF <= 64) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else lds_barrier();
+}
+
 template <int Q, int LOGM, int DIAG>
 __device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid, const float2 *twc,
                                            const float2 *twf, int shift, int tw_scale) {
@@ -116,9 +129,9 @@ __device__ __forceinline__ void run_passes(float2 (&v)[16], float2 *buf, int tid
         butterflies<Q, LOGM>(v, tid, twc, twf, shift, tw_scale);
         if constexpr (Q + 1 < G::NPASS) {
             lds_write<Q, LOGM>(v, buf, tid);
-            lds_barrier();
+            exchange_sync<LOGM>();
             lds_read<Q + 1, LOGM>(v, buf, tid);
-            lds_barrier();
+            exchange_sync<LOGM>();
             run_passes<Q + 1, LOGM, DIAG>(v, buf, tid, twc, twf, shift, tw_scale);
         }
     }
