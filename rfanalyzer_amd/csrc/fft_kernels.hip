@@ -548,6 +548,12 @@ __global__ void state_combine_kernel(StateLaunch a, int chunks) {
 // all CH chunks of frames; the chunk summaries meet in LDS and the block folds
 // them in frame order into peaks / EMA (same algebra as state_combine_kernel),
 // so no summary buffer round trip and no second launch.
+#ifndef RFA_STATE_BUF
+#define RFA_STATE_BUF 1
+#endif
+#ifndef RFA_STATE_UNROLL
+#define RFA_STATE_UNROLL 4
+#endif
 template <int CH>
 __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chunk_len) {
     constexpr int TPC = 256 / CH, BPB = 4 * TPC;  // threads per chunk, bins per block
@@ -568,13 +574,28 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
 #pragma unroll
         for (int k = 0; k < 4; k++) pk[k] = emi[k] = -INFINITY, b[k] = 0.0f, restart[k] = false;
         float am = 1.0f;
-#pragma unroll 4  // frames in flight per thread (profiles/r02c/state_unroll_ab.txt)
-        for (int f = f0; f < f1; f++) {
-            const float4 x4 = *reinterpret_cast<const float4 *>(state_row(a, f) + bin);  // storage positions
+        auto step = [&](float4 x4) {
             const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
             for (int k = 0; k < 4; k++) state_step(pk[k], emi[k], b[k], restart[k], xs[k], al);
             am *= keep;
+        };
+        if (RFA_STATE_BUF && a.ring_rows > 0 && (long long)a.ring_rows * a.n * 4 < (1ll << 31)) {
+            // ring rows: the chunk's first row once, then one row down per frame with the wrap
+            // (FftProcessor.kt:226-227 writeIndex--), as 32-bit buffer offsets -- not a modulo
+            // and a 64-bit address per frame (four chunks share a wave, so they are per lane)
+            const unsigned rowb = (unsigned)a.n * 4u;
+            const rsrc_t rs = make_rsrc(a.rows, (unsigned)a.ring_rows * rowb);
+            int rr = (a.ring_base - f0) % a.ring_rows;
+            if (rr < 0) rr += a.ring_rows;
+#pragma unroll RFA_STATE_UNROLL
+            for (int f = f0; f < f1; f++) {
+                step(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((unsigned)rr * rowb + (unsigned)bin * 4u), 0, 0)));
+                rr = rr == 0 ? a.ring_rows - 1 : rr - 1;
+            }
+        } else {
+#pragma unroll 4  // frames in flight per thread (profiles/r02c/state_unroll_ab.txt)
+            for (int f = f0; f < f1; f++) step(*reinterpret_cast<const float4 *>(state_row(a, f) + bin));  // storage positions
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) part[c][4 * l + k] = make_float4(pk[k], restart[k] ? -1.0f : am, b[k], emi[k]);

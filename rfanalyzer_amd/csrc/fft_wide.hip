@@ -33,6 +33,9 @@ namespace rfa {
 // finished its own items keeps polling for chunks still in flight (s_memrealtime ticks of
 // 10 ns) before it leaves the rest to the finish kernel
 [[maybe_unused]] constexpr int kSc1 = 16;
+#ifndef RFA_RING_SC1
+#define RFA_RING_SC1 1  // 16-B ring tile stores write-through (profiles/r04/ring_store_sc1_ab.txt; A/B: 0)
+#endif
 #ifndef RFA_IGS_WAIT
 #define RFA_IGS_WAIT 0  // 4000 (40 us) cost the kernel +45 us: every workgroup polled for the last chunks
 #endif
@@ -978,7 +981,8 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
                                     buf_store_f32(d[e], row_rs, vo,
                                                   ((ors * (t * (M / G::R2)) + on / 2) & (on - 1)) * 4);
                             }
-                            buf_store_f32x4(d[0], d[1], d[2], d[3], ring_rs, tvo, j * 1024);
+                            if constexpr (RFA_RING_SC1) buf_store_f32x4(d[0], d[1], d[2], d[3], ring_rs, tvo, j * 1024);
+                            else buf_store_f32x4_wb(d[0], d[1], d[2], d[3], ring_rs, tvo, j * 1024);
                         }
                     };
                     if (a.rows) store_tiles(std::true_type{});
