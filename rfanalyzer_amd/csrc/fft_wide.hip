@@ -45,13 +45,18 @@ constexpr unsigned long long kStWaitTicks = RFA_IGS_WAIT;
                         // the last chunk's units then ran serially on the last workgroups)
 #endif
 
+#ifndef RFA_WIDE_KR1
+#define RFA_WIDE_KR1 0
+#endif
 template <int LOGM, int PT>
 struct WGeo {
     static constexpr int M = 1 << LOGM;
     static constexpr int TPF = M / PT;           // threads per sub-FFT (PT points per thread)
     static constexpr int THREADS = TPF < 256 ? 256 : TPF;
     static constexpr int SLOTS = THREADS / TPF;  // sub-FFTs per workgroup
-    static constexpr int HALF = M / 2;           // exchange buffer (float2) per slot ...
+    // exchange buffer (float2) per slot: M / 2, two rounds per exchange; A/B RFA_WIDE_KR1 (8 K): the
+    // whole M, one round (half the barriers, 2 instead of 4 workgroups per CU)
+    static constexpr int HALF = (RFA_WIDE_KR1 && LOGM == 13) ? M : M / 2;
     static constexpr int HALFP = HALF + HALF / 32;  // ... with one float2 of padding per 32
     static constexpr int R1 = LOGM >= 14 ? 32 : 16;  // radix of pass 1 (pass 0: 32)
     static constexpr int R2 = M / (32 * R1);          // radix of pass 2: 16 (8 K, 16 K) or 32 (32 K)
@@ -588,7 +593,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     constexpr bool QSTB = STG && RS == 1 && (dif || FMT == 3) && !COMPLEX_OUT;
     constexpr int QB_BYTES = (M / 2) * 8;
     constexpr int QP = M / 4 + M / 128;              // region A (padded quarter, float2)
-    constexpr int KR = SPLIT ? 4 : 2;                // exchange rounds
+    constexpr int KR = SPLIT ? 4 : ((RFA_WIDE_KR1 && LOGM == 13) ? 1 : 2);  // exchange rounds
     constexpr int HALF_BYTES = M * RS * BPS / 2;
     constexpr int JS = SPLIT ? -(QP * 8) / BPS : 0;  // raw-element offset of the second half (A) from B
     static_assert(!SPLIT || (G::HALFP - QP) * 8 >= HALF_BYTES, "region B holds half a frame");
