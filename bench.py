@@ -375,14 +375,15 @@ def demod_companion(torch, device, steps, samples=1 << 26):
 
 
 def host_fed_run(torch, device, n, fmt, frames, calls, window="blackman", avg="ema", peak=True, ring_rows=500,
-                 host_batches=2, seed=7):
+                 host_batches=2, seed=7, state_out=False):
     """Host-fed end to end (SURVEY.md §7 "Host feed vs device throughput"; the reference path
     is host-fed by construction: FileIQSource.java:318-369 -> Scheduler.kt:252-279 ->
     FftProcessor.kt:111-140).  The raw IQ batches sit in pinned host memory; each call's batch
     is copied H2D on a second stream into one of two device buffers (double buffering: the
     copy of batch i+1 runs while batch i is processed), then rfa_process() reads it into the
     device ring + peak / EMA state only (no rows back).  Returns wall-clock Msamples/s over
-    `calls` calls, the H2D-only rate of the same copies, and the per-call split."""
+    `calls` calls, the H2D-only rate of the same copies, and the per-call split (state_out: also
+    the engine's peaks / EMA after the run, for tests/test_host_feed.py)."""
     import rfanalyzer_amd
 
     st = torch.cuda.current_stream(device)
@@ -425,12 +426,13 @@ def host_fed_run(torch, device, n, fmt, frames, calls, window="blackman", avg="e
     run(calls, process=False)
     torch.cuda.synchronize(device)
     el_copy = time.perf_counter() - t0
+    state = {"peaks": eng.peaks(), "ema": eng.ema()} if state_out else {}
     eng.close()
     samples = calls * frames * n
     return {"value": round(samples / el / 1e6, 2), "unit": "Msamples/s", "ms_per_call": round(el / calls * 1e3, 4),
             "h2d_GBps": round(calls * nbytes / el_copy / 1e9, 2),
             "h2d_only_ms_per_call": round(el_copy / calls * 1e3, 4), "bytes_per_call": nbytes,
-            "frames_per_call": frames, "calls": calls}
+            "frames_per_call": frames, "calls": calls, **state}
 
 
 def c_call_cost(calls=4000):
