@@ -257,8 +257,9 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
             const size_t fb = (size_t)n * 2;
             if (ensure_device_buffer(h, (void **)&h->d_dit_in, &h->d_dit_in_cap, (size_t)h->dit_frames * fb))
                 return hipErrorOutOfMemory;
-            hipError_t e = hipMemcpy2DAsync(h->d_dit_in, fb, A.in, (size_t)A.frame_stride, fb, cnt, hipMemcpyDeviceToDevice,
-                                            a.stream);
+            // (one frame: its stride is not validated against the frame size and is not used)
+            const size_t sp = cnt > 1 ? (size_t)A.frame_stride : fb;
+            hipError_t e = hipMemcpy2DAsync(h->d_dit_in, fb, A.in, sp, fb, cnt, hipMemcpyDeviceToDevice, a.stream);
             if (e != hipSuccess) return e;
             A.in = h->d_dit_in;
             A.frame_stride = (long long)fb;

@@ -196,10 +196,12 @@ def test_large_n_seams(rfa, n):
 
 @pytest.mark.parametrize("fmt", ["s8", "u8"])
 def test_large_n_front_kernel_alignment_paths(rfa, fmt):
-    """N = 1 M, 8-bit input: 16-byte aligned frames take the pipelined persistent front
-    kernel (LDS-DMA tiles), a misaligned device pointer the one-block-per-tile kernel.
-    Both do the same fp32 operations in the same order, so the rows are bit-identical,
-    and both match the oracle; 7 frames over 6 frame groups exercises the uneven split."""
+    """N = 1 M, 8-bit input: 16-byte aligned frames go straight to the pipelined persistent
+    front kernel (LDS-DMA tiles); a misaligned device pointer is first copied 16-B aligned
+    (round 5), so the same kernel rounds them and the rows are bit-identical; both match the
+    oracle; 7 frames over 6 frame groups exercises the uneven split.  A single misaligned frame
+    with a frame stride smaller than the frame (not validated for one frame, so the copy must
+    not use it) gives the same first row."""
     torch = pytest.importorskip("torch")
 
     n, frames = 1 << 20, 7
@@ -215,7 +217,12 @@ def test_large_n_front_kernel_alignment_paths(rfa, fmt):
             e.process_tensor(buf[off:off + raw.size], frames, 0, rows)
             torch.cuda.synchronize()
             out.append(rows.cpu().numpy())
+        one = torch.empty((1, n), dtype=torch.float32, device="cuda")
+        e.process_device(buf.data_ptr() + 2, 1, 2, one.data_ptr())  # buf holds the data at offset 2
+        torch.cuda.synchronize()
+        single = one.cpu().numpy()
     np.testing.assert_array_equal(out[0], out[1])
+    np.testing.assert_array_equal(single[0], out[0][0])
     assert gu.db_diff(out[0], ref) <= gu.DB_TOL
     gu.assert_same_peak_bins(out[0], np.argmax(ref, 1))
 
