@@ -53,7 +53,7 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
     except ImportError:
         return
     log = gu.PARITY_LOG
-    if not log:
+    if not (log or gu.FULL_ROW_LOG or gu.NOTES):
         return
     tr = terminalreporter
     tr.write_sep("-", "dB parity (tests/golden_util.py db_stats)")
