@@ -94,20 +94,66 @@ def test_config2_no_worse_than_reference(rfa, seed):
     data = signals.frames_bytes(n, b, "f32", seed, tones=((1000 / n, 0.5), (5000.5 / n, 0.05)), noise=0.01)
     with _engine(rfa, n, "f32", "hann", ring_rows=0) as e:
         rows = e.process(data, b)
-    ref64 = oracle.spectrum_rows(data, oracle.IN_F32_INTERLEAVED, n, b, None, oracle.WIN_HANN)
-    ref = oracle.ref_spectrum_rows(data, oracle.IN_F32_INTERLEAVED, n, b, None, oracle.WIN_HANN)
+    _no_worse_than_reference(f"config 2 seed {seed:2d}", rows, data, oracle.IN_F32_INTERLEAVED, n, b, oracle.WIN_HANN)
+
+
+def _no_worse_than_reference(label, rows, data, fmt_code, n, b, win, counts_vs_ref=True):
+    """The bars of test_config3_no_worse_than_reference for any batch: deep-bin error vs float64
+    at most pffft's; worst bin inside DB_TOL_BATCH_MAX or pffft's own worst bin; identical peak
+    bins; and (counts_vs_ref) the share of bins beyond 0.01 dB and the 1e-6 tail quantile at most
+    pffft's.  Without counts_vs_ref the share has the absolute round-4 bar BATCH_EXCEED_SHARE
+    instead and the quantile is printed only: on a 2.1 M-bin (config 4) or 16.8 M-bin (config 5)
+    batch both are counts of 0-7 bins, which flip between the two transforms from capture to
+    capture while the deep-bin error (the population those bins are drawn from) stays 0.66-0.81
+    of pffft's.  Prints one NOTES line."""
+    ref64 = oracle.spectrum_rows(data, fmt_code, n, b, None, win)
+    ref = oracle.ref_spectrum_rows(data, fmt_code, n, b, None, win)
     sh_l, sh_p = gu.exceed_fraction(rows, ref64), gu.exceed_fraction(ref, ref64)
     de_l, de_p = gu.deep_bin_error(rows, ref64), gu.deep_bin_error(ref, ref64)
     mx_l, mx_p = gu.full_row_diff(rows, ref64, bar=None), gu.full_row_diff(ref, ref64, bar=None)
     q_l, q_p = gu.tail_quantile(rows, ref64), gu.tail_quantile(ref, ref64)
-    gu.NOTES.append(f"config 2 seed {seed:2d} vs float64, librfa / pffft: share > {gu.DB_TOL} dB {sh_l:.2e} / {sh_p:.2e}; "
+    gu.NOTES.append(f"{label} vs float64, librfa / pffft: share > {gu.DB_TOL} dB {sh_l:.2e} / {sh_p:.2e}; "
                     f"deep-bin error {de_l:.3e} / {de_p:.3e} (ratio {de_l / de_p:.2f}); 1e-6 quantile {q_l:.4f} / "
                     f"{q_p:.4f} dB; max {mx_l:.4f} / {mx_p:.4f} dB")
-    assert sh_l <= sh_p, (sh_l, sh_p)
     assert de_l <= de_p, (de_l, de_p)
-    assert q_l <= q_p, (q_l, q_p)
+    if counts_vs_ref:
+        assert sh_l <= sh_p, (sh_l, sh_p)
+        assert q_l <= q_p, (q_l, q_p)
+    else:
+        assert sh_l <= gu.BATCH_EXCEED_SHARE, sh_l
     assert mx_l <= max(gu.DB_TOL_BATCH_MAX, mx_p), (mx_l, mx_p)
     gu.assert_same_peak_bins(rows, np.argmax(ref64, 1))
+
+
+@pytest.mark.parametrize("seed", gu.CONFIG3_SEEDS)
+def test_config4_no_worse_than_reference(rfa, seed):
+    """BASELINE config 4's batch (256 concurrent s8 frames of 8192 points, Blackman) on four
+    captures: librfa's deep-bin rounding error no worse than the reference's pffft, plus the
+    absolute share / worst-bin bars (_no_worse_than_reference, counts_vs_ref=False)."""
+    if not oracle.ref_available():
+        pytest.skip("reference pffft build (oracle/_ref) absent")
+    n, b = 8192, 256
+    data = signals.frames_bytes(n, b, "s8", seed, tones=((0.1234, 0.4), (-0.377, 0.01)), noise=0.05)
+    with _engine(rfa, n, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(data, b)
+    _no_worse_than_reference(f"config 4 seed {seed:2d}", rows, data, oracle.IN_S8, n, b, oracle.WIN_BLACKMAN,
+                             counts_vs_ref=False)
+
+
+@pytest.mark.parametrize("seed", gu.CONFIG3_SEEDS)
+def test_config5_no_worse_than_reference(rfa, seed):
+    """BASELINE config 5's stream shape (1 M-point s8 frames, Blackman; the decimation-in-
+    frequency pair of §5.5) over 16 frames of four captures: librfa's deep-bin rounding error no
+    worse than the reference's pffft, plus the absolute share / worst-bin bars
+    (_no_worse_than_reference, counts_vs_ref=False)."""
+    if not oracle.ref_available():
+        pytest.skip("reference pffft build (oracle/_ref) absent")
+    n, b = 1 << 20, 16
+    data = signals.frames_bytes(n, b, "s8", seed, tones=((0.1234, 0.4), (-0.377, 0.01)), noise=0.05)
+    with _engine(rfa, n, "s8", "blackman", ring_rows=0) as e:
+        rows = e.process(data, b)
+    _no_worse_than_reference(f"config 5 seed {seed:2d}", rows, data, oracle.IN_S8, n, b, oracle.WIN_BLACKMAN,
+                             counts_vs_ref=False)
 
 
 def test_frame_stride_matches_packet_framing(rfa):
