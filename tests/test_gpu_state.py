@@ -298,6 +298,32 @@ def test_config3_state_at_size(rfa, n, ring_rows, batches):
                 assert np.all(ring[[(-g) % ring_rows for g in range(f, ring_rows)]] == -9999)
 
 
+def test_state_over_a_ring_beyond_2_gib(rfa):
+    """state_fused_kernel walks a ring under 2 GiB by 32-bit buffer offsets and a larger one by
+    flat addresses (fft_kernels.hip, RFA_STATE_BUF).  At N = 64 K a 8200-row ring is 2.15 GB:
+    the same frames through it and through a 500-row ring give bit-identical peaks and EMA
+    (same chunking, same arithmetic, only the addressing differs), and both match the
+    oracle."""
+    n, batches, alpha = 65536, (137, 300), 0.1
+    total = sum(batches)
+    data, rows = _cfg3_rows(n, total, 3)
+    fb = 2 * n
+    out = []
+    for ring_rows in (500, 8200):
+        with rfa.SpectrumEngine(n, "blackman", "s8", avg="ema", ema_alpha=alpha, peak_hold=True,
+                                ring_rows=ring_rows) as e:
+            e.set_tuning(433_920_000, 20_000_000)
+            f = 0
+            for b in batches:
+                e.process(data[f * fb:(f + b) * fb], b, rows=False)
+                f += b
+            out.append((e.peaks(), e.ema()))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert gu.db_diff(out[1][0], rows[:total].max(0)) <= gu.DB_TOL
+    assert gu.db_diff(out[1][1], processor.ema_batch(rows[:total], alpha)) <= gu.DB_TOL
+
+
 @pytest.mark.parametrize("n,batches", [(262144, (3, 9, 2)), (524288, (5, 6)), (1048576, (1, 7, 4))])
 def test_column_order_ring_state_tiles(rfa, n, batches):
     """N >= 256 K keeps the ring in column order (RS = N / 32 K blocks); the peak / EMA
