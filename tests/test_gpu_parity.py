@@ -271,9 +271,10 @@ def test_large_n_seams(rfa, n):
     dsp.close()
 
 
+@pytest.mark.parametrize("n,frames", [(1 << 20, 7), (1 << 18, 9)])
 @pytest.mark.parametrize("fmt", ["s8", "u8"])
-def test_large_n_front_kernel_alignment_paths(rfa, fmt):
-    """N = 1 M, 8-bit input: 16-byte aligned frames go straight to the pipelined persistent
+def test_large_n_front_kernel_alignment_paths(rfa, fmt, n, frames):
+    """N = 1 M and 256 K, 8-bit input: 16-byte aligned frames go straight to the pipelined persistent
     front kernel (LDS-DMA tiles); a misaligned device pointer is first copied 16-B aligned
     (round 5), so the same kernel rounds them and the rows are bit-identical; both match the
     oracle; 7 frames over 6 frame groups exercises the uneven split.  A single misaligned frame
@@ -281,7 +282,6 @@ def test_large_n_front_kernel_alignment_paths(rfa, fmt):
     not use it) gives the same first row."""
     torch = pytest.importorskip("torch")
 
-    n, frames = 1 << 20, 7
     data = signals.frames_bytes(n, frames, fmt, seed=77, tones=((0.0123, 0.3), (-0.41, 0.02)), noise=0.04)
     raw = np.frombuffer(data, np.uint8)
     ref = oracle.spectrum_rows(data, signals.FORMATS[fmt], n, frames, None, oracle.WIN_BLACKMAN)
