@@ -27,6 +27,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORC_PATH = os.path.join(HERE, "liborc.so")
 REF_PATH = os.path.join(HERE, "_ref", "libpffft_ref.so")
+# diagnostic only: the same pffft.c with exact (double-angle) twiddle tables, exact_twiddle.c
+EXACT_PATH = os.path.join(HERE, "_ref", "libpffft_exact.so")
 
 IN_S8, IN_U8, IN_S16LE, IN_F32_INTERLEAVED, IN_F32_PLANAR = range(5)
 WIN_BLACKMAN, WIN_HANN, WIN_NONE = range(3)
@@ -34,6 +36,7 @@ BYTES_PER_SAMPLE = {IN_S8: 2, IN_U8: 2, IN_S16LE: 4, IN_F32_INTERLEAVED: 8, IN_F
 
 _orc = None
 _ref = None
+_exact = None
 
 _fp = ctypes.POINTER(ctypes.c_float)
 
@@ -76,6 +79,25 @@ def ref() -> ctypes.CDLL:
                                  _fp, ctypes.c_int, _fp]
         _ref = lib
     return _ref
+
+
+def exact_available() -> bool:
+    return os.path.exists(EXACT_PATH)
+
+
+def exact() -> ctypes.CDLL:
+    """The reference's pffft with its twiddle tables recomputed from exact angles (a diagnostic
+    of pffft's own float-argument twiddles, pffft.c:1140,1156,1160-1161,1261; never the oracle)."""
+    global _exact
+    if _exact is None:
+        if not os.path.exists(EXACT_PATH):
+            raise FileNotFoundError(f"{EXACT_PATH} missing (reference pffft not built)")
+        lib = ctypes.CDLL(EXACT_PATH)
+        lib.exact_fft_ordered.argtypes = [_fp, ctypes.c_int, _fp]
+        lib.exact_fft_logmag.argtypes = [_fp, ctypes.c_int, _fp]
+        lib.exact_max_change.restype = ctypes.c_double
+        _exact = lib
+    return _exact
 
 
 def _f32ptr(a: np.ndarray):
@@ -149,8 +171,9 @@ def ref_fft_ordered(interleaved: np.ndarray) -> np.ndarray:
 
 
 def ref_spectrum_rows(data, fmt: int, n: int, n_frames: int, frame_stride_bytes: int | None = None,
-                      win: int | np.ndarray | None = WIN_BLACKMAN) -> np.ndarray:
-    """Same as spectrum_rows but with the reference's own pffft as the FFT."""
+                      win: int | np.ndarray | None = WIN_BLACKMAN, exact_twiddles: bool = False) -> np.ndarray:
+    """Same as spectrum_rows but with the reference's own pffft as the FFT (exact_twiddles: the
+    diagnostic build whose twiddle tables come from exact angles, exact_twiddle.c)."""
     buf = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
     bps = BYTES_PER_SAMPLE[fmt]
     if frame_stride_bytes is None:
@@ -163,5 +186,10 @@ def ref_spectrum_rows(data, fmt: int, n: int, n_frames: int, frame_stride_bytes:
     for f in range(n_frames):
         frame = buf[f * frame_stride_bytes: f * frame_stride_bytes + n * bps]
         re, im = convert(frame, fmt, n)
-        out[f] = ref_fft_logmag(windowed_interleaved(re, im, w))
+        x = windowed_interleaved(re, im, w)
+        if exact_twiddles:
+            if exact().exact_fft_logmag(_f32ptr(x), n, _f32ptr(out[f])) != 0:
+                raise ValueError("exact-twiddle pffft setup failed")
+        else:
+            out[f] = ref_fft_logmag(x)
     return out

@@ -69,14 +69,6 @@ struct rfa_handle {
     float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
     int state_chunks = 1;
     int state_fused = 1;              // single-launch chunked scan (A/B builds: RFA_STATE_FUSED=0 two kernels)
-    // in-grid state (N = 64 K, rows in the ring; fft_kernels.h FftLaunch st_*):
-    // chunk counters + ticket counter, per-unit generation stamps, the call generation
-    unsigned *d_st_cnt = nullptr;     // [kStCntWords]: chunk counts, chunk tickets, diagnostics
-    unsigned *d_st_done = nullptr;    // [kStMaxChunks][n >> 10]
-    unsigned st_gen = 0;
-    bool st_dirty = false;            // counters may be non-zero (a main launch without its state launch)
-    bool st_last = false;             // the last call took the in-grid path (rfa_debug_igs)
-    int igs = RFA_IGS;                // in-grid state (A/B builds built with -DRFA_IGS=1; env RFA_IGS=0 off)
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -579,18 +571,6 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
         if (h->state_chunks > 1 &&
             hipMalloc(&h->d_state_part, (size_t)h->state_chunks * n * sizeof(float4)) != hipSuccess)
             return bail(RFA_ERR_NOMEM);
-#ifdef RFA_AB_BUILD
-        if (const char *d = std::getenv("RFA_IGS")) h->igs = std::atoi(d);
-#endif
-        if (RFA_IGS && logn == 16 && h->d_state_part) {  // in-grid state of the 64 K staged kernels
-            const size_t done_words = (size_t)rfa::kStMaxChunks * (n / rfa::kStRange);
-            if (hipMalloc(&h->d_st_cnt, rfa::kStCntWords * sizeof(unsigned)) != hipSuccess ||
-                hipMalloc(&h->d_st_done, done_words * sizeof(unsigned)) != hipSuccess)
-                return bail(RFA_ERR_NOMEM);
-            if (hipMemset(h->d_st_cnt, 0, rfa::kStCntWords * sizeof(unsigned)) != hipSuccess ||
-                hipMemset(h->d_st_done, 0, done_words * sizeof(unsigned)) != hipSuccess)
-                return bail(RFA_ERR_HIP);
-        }
     }
     if (hipMalloc(&h->d_boxcar, n * sizeof(float)) != hipSuccess) return bail(RFA_ERR_NOMEM);
     if (clear_ring(h) || reset_peaks_ema(h)) return bail(RFA_ERR_HIP);
@@ -627,8 +607,6 @@ int rfa_destroy(rfa_handle *h) {
     hipFree(h->d_peaks);
     hipFree(h->d_ema);
     hipFree(h->d_state_part);
-    hipFree(h->d_st_cnt);
-    hipFree(h->d_st_done);
     hipFree(h->d_chan);
     hipFree(h->d_draw);
     hipFree(h->d_colors);
@@ -668,26 +646,6 @@ int rfa_get_stream(const rfa_handle *h, void **stream) {
     *stream = (void *)h->stream;
     return RFA_OK;
 }
-
-#ifdef RFA_AB_BUILD
-// A/B builds only (not in rfa.h): in-grid state diagnostics after a synchronise --
-// out[0] = call generation, out[1] = units of the last call stamped by the main kernel,
-// out[2] = 1 if the last call took the in-grid path, out[3..3+kStMaxChunks] = the counters
-extern "C" RFA_API int rfa_debug_igs(rfa_handle *h, unsigned *out) {
-    if (!h || !out) return RFA_ERR_INVALID;
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return RFA_ERR_HIP;
-    out[0] = h->st_gen;
-    out[1] = 0;
-    out[2] = h->st_last ? 1u : 0u;
-    if (!h->d_st_done) return RFA_OK;
-    std::vector<unsigned> done((size_t)rfa::kStMaxChunks * (h->n / rfa::kStRange));
-    if (hipMemcpy(done.data(), h->d_st_done, done.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return RFA_ERR_HIP;
-    for (unsigned d : done) out[1] += d == h->st_gen;
-    if (hipMemcpy(out + 3, h->d_st_cnt, rfa::kStCntWords * 4, hipMemcpyDeviceToHost) != hipSuccess)
-        return RFA_ERR_HIP;
-    return RFA_OK;
-}
-#endif
 
 int rfa_synchronize(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
@@ -789,28 +747,6 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
         a.ring_logrs = h->ring_logrs;
     }
-    // in-grid state: the 64 K staged kernel summarises complete frame chunks
-    // between its work items; state_fused_kernel (same chunking: rfa::state_fused_plan) folds
-    // them and computes whatever the grid left.  Rows in the ring only (the units read it).
-    int st_ch = 0, st_len = 0;
-    h->st_last = false;
-    const bool igs = h->igs && h->d_st_cnt && need_state && rows_in_ring && h->logn == 16 &&
-                     (size_t)h->ring_rows * (size_t)n * 4 < ((size_t)1 << 31) &&
-                     rfa::state_fused_plan(n, (int)n_frames, h->state_chunks, h->state_fused, &st_ch, &st_len) &&
-                     st_len <= 32;
-    if (igs) {
-        if (h->st_dirty)  // a previous main launch lost its state launch: counters not reset
-            HIPCHK(h, hipMemsetAsync(h->d_st_cnt, 0, rfa::kStDbg * sizeof(unsigned), h->stream));
-        h->st_gen++;
-        a.st_part = h->d_state_part;
-        a.st_cnt = h->d_st_cnt;
-        a.st_done = h->d_st_done;
-        a.st_gen = h->st_gen;
-        a.st_chunk_len = st_len;
-        a.st_alpha = h->cfg.ema_alpha;
-        h->st_dirty = true;
-        h->st_last = true;
-    }
     int rc = launch_main(h, a);
     if (rc) return rc;
     if (need_state || need_chan) {
@@ -833,13 +769,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             s.rows = state_rows;
             s.row_stride = n;
         }
-        if (igs) {
-            s.done = h->d_st_done;
-            s.gen = h->st_gen;
-            s.cnt = h->d_st_cnt;
-        }
         if (need_state) HIPCHK(h, rfa::launch_state(s));
-        if (igs) h->st_dirty = false;
         if (need_chan) {
             // means, then (channels wider than 16384 bins) the per-span partial sums
             const int spans = rfa::channel_mean_spans(chan_last - chan_first);

@@ -109,29 +109,11 @@ struct FftLaunch {
     int phase_ticks = 0;  // A/B builds (RFA_PHASE_NS): persistent workgroups of the second half of
                           // the grid start this many 10-ns ticks late (phase offset between the
                           // two workgroups of a CU)
-    // In-grid peak / EMA state (N = 64 K staged kernels, rows in the ring).
-    // A work item adds 1 to st_cnt[chunk of its frame] once its ring stores are written
-    // through; between items a workgroup takes a unit (chunk c, 1024 storage positions) of a
-    // complete chunk, writes the chunk summary to st_part[c][pos] (state_partial_kernel's
-    // float4) and stamps st_done[unit] = st_gen; state_finish (state_fused_kernel with these
-    // fields) folds the summaries, computes the units nobody took, and resets the counters.
-    // Never waits: a unit is taken only when its chunk is already complete.
-    float4 *st_part = nullptr;
-    unsigned *st_cnt = nullptr;   // [kStCntWords]: items done per chunk, unit tickets per chunk
-    unsigned *st_done = nullptr;  // [kStMaxChunks][n >> 10]
-    unsigned st_gen = 0;
-    int st_chunk_len = 0;  // frames per chunk (<= 32); 0: in-grid state off
-    float st_alpha = 0.f;
+    // persistent grids: workgroups per CU x this many CUs (0: every CU of the device; a
+    // CU-masked stream's CU count, engine.hip pipelined state)
+    int cus = 0;
     hipStream_t stream = nullptr;
 };
-constexpr int kStMaxChunks = 32;
-// st_cnt words: [kStMaxChunks] items done per chunk, [kStMaxChunks] unit tickets per chunk,
-// then kStDbg.. diagnostics (RFA_IGS_DEBUG)
-constexpr int kStDbg = 2 * kStMaxChunks, kStCntWords = kStDbg + 8;
-#ifndef RFA_IGS
-#define RFA_IGS 0  // in-grid state compiled in (A/B builds only: a measured loss)
-#endif
-constexpr int kStRange = 4096;  // storage positions per in-grid unit (four per thread of the 32 K workgroup)
 
 // Fused convert -> window -> FFT -> log-mag/shift -> rows/ring (or complex out).
 hipError_t launch_fft(const FftLaunch &a);
@@ -202,11 +184,6 @@ struct StateLaunch {
     float4 *part = nullptr;  // chunk summaries [max_chunks][n] (null: sequential kernel only)
     int max_chunks = 1;
     int fused = 1;           // single-launch chunked scan (RFA_STATE_FUSED=0: partial + combine kernels)
-    // in-grid summaries of the main kernel (FftLaunch st_*): chunk c of the 1024-position range
-    // r is read from part[c][pos] when done[c][r] == gen; cnt's kStDbg counter words are reset
-    const unsigned *done = nullptr;
-    unsigned gen = 0;
-    unsigned *cnt = nullptr;
     hipStream_t stream = nullptr;
 };
 hipError_t launch_state(const StateLaunch &a);

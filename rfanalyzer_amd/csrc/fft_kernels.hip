@@ -331,7 +331,7 @@ static hipError_t launch_one(const FftLaunch &a) {
     const int items = (RS == 1) ? (a.n_frames + G::SLOTS - 1) / G::SLOTS : ((a.n_frames + 7) / 8) * 8 * RS;
     if (items <= 0) return hipSuccess;
     int grid = items;
-    if (Persist<LOGM, RS>::value) grid = std::min(items, g_cus * per_cu);
+    if (Persist<LOGM, RS>::value) grid = std::min(items, (a.cus > 0 ? a.cus : g_cus) * per_cu);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), lds, a.stream, a);
     return hipGetLastError();
 }
@@ -560,13 +560,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
     __shared__ float4 part[CH][BPB];
     const int c = threadIdx.x / TPC, l = threadIdx.x % TPC;
     const int bin = blockIdx.x * BPB + 4 * l;
-    if (a.cnt && blockIdx.x == 0 && threadIdx.x < kStDbg) a.cnt[threadIdx.x] = 0u;  // in-grid counters
-    // chunk c of this block's bins summarised in-grid by the main kernel (FftLaunch st_*):
-    // the same float4 state_step forms, so which kernel formed it does not change the result
-    if (a.done && a.done[c * (a.n / kStRange) + blockIdx.x * BPB / kStRange] == a.gen) {
-#pragma unroll
-        for (int k = 0; k < 4; k++) part[c][4 * l + k] = a.part[(size_t)c * a.n + bin + k];
-    } else {
+    {
         const int f0 = c * chunk_len, f1 = min(a.n_frames, f0 + chunk_len);
         const float al = a.ema_alpha, keep = 1.0f - al;
         float pk[4], emi[4], b[4];
@@ -650,12 +644,11 @@ hipError_t launch_state(const StateLaunch &a) {
     int chunks = a.part ? std::min(a.max_chunks, (a.n_frames + 7) / 8) : 1;
     int ch = 0, len = 0;
     if (a.part && state_fused_plan(a.n, a.n_frames, a.max_chunks, a.fused, &ch, &len)) {
-        // single-launch form: CH = 8, 16 or 32 chunks (with a.done: also the in-grid fold)
+        // single-launch form: CH = 8, 16 or 32 chunks
         auto k = ch == 32 ? state_fused_kernel<32> : ch == 16 ? state_fused_kernel<16> : state_fused_kernel<8>;
         hipLaunchKernelGGL(k, dim3(a.n / (1024 / ch)), dim3(256), 0, a.stream, a, len);
         return hipGetLastError();
     }
-    if (a.done) return hipErrorInvalidValue;  // in-grid summaries need the fused fold
     if (chunks > 1) {
         const int len = (a.n_frames + chunks - 1) / chunks;
         chunks = (a.n_frames + len - 1) / len;

@@ -28,23 +28,12 @@
 
 namespace rfa {
 
-// in-grid state (fft_wide_kernel IGS): sc1 cache policy of a raw buffer load (gfx950: bit 4 of
-// the aux operand; the load then bypasses the CU's L1), and how long a workgroup that has
-// finished its own items keeps polling for chunks still in flight (s_memrealtime ticks of
-// 10 ns) before it leaves the rest to the finish kernel
+// sc1 cache policy of a raw buffer access (gfx950: bit 4 of the aux operand: the line
+// bypasses / leaves the CU's L1)
 [[maybe_unused]] constexpr int kSc1 = 16;
 #ifndef RFA_RING_SC1
 #define RFA_RING_SC1 1  // 16-B ring tile stores write-through (profiles/r04/ring_store_sc1_ab.txt; A/B: 0)
 #endif
-#ifndef RFA_IGS_WAIT
-#define RFA_IGS_WAIT 0  // 4000 (40 us) cost the kernel +45 us: every workgroup polled for the last chunks
-#endif
-constexpr unsigned long long kStWaitTicks = RFA_IGS_WAIT;
-#ifndef RFA_IGS_TAIL
-#define RFA_IGS_TAIL 1  // units a workgroup may take after its last item (-1: until none is ready;
-                        // the last chunk's units then ran serially on the last workgroups)
-#endif
-
 #ifndef RFA_WIDE_KR1
 #define RFA_WIDE_KR1 0
 #endif
@@ -474,66 +463,6 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     }
 }
 
-#if RFA_IGS
-// In-grid state unit (fft_wide_kernel IGS, N = 64 K): chunk c's summary (state_step, the
-// float4 of fft_kernels.hip state_partial_kernel) over kStRange storage positions, four per
-// thread, written to st_part[c][pos].  Row loads are 16-B sc1 loads (the rows were written
-// through by other CUs), 16 frames in flight.  noinline: its registers do not join the FFT
-// body's allocation (inlined, they lifted the kernel's SGPR spills 16 -> 74).
-__device__ __attribute__((noinline)) void st_unit(unsigned karg_lo, unsigned karg_hi, int t_) {
-    using KArg = const __attribute__((address_space(4))) FftLaunch;
-    // (readfirstlane returns int: widen through unsigned, or a low half >= 2^31 sign-extends
-    // over the high half)
-    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane(karg_lo);
-    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane(karg_hi);
-    KArg *k = (KArg *)(((unsigned long long)hi << 32) | lo);
-    constexpr int n = 1 << 16, ranges = n / kStRange, IF = 16;
-    const int t = __builtin_amdgcn_readfirstlane(t_);
-    const int c = t / ranges, pos = (t - c * ranges) * kStRange + 4 * (int)(threadIdx.x & 1023);
-    const int cl = k->st_chunk_len, f0 = c * cl, nf = min(k->n_frames - f0, cl);
-    const int rows = k->ring_rows;
-    int rr = (k->ring_base - f0) % rows;
-    if (rr < 0) rr += rows;
-    const rsrc_t rs = make_rsrc(k->ring, (unsigned)rows * (unsigned)(n * 4));
-    const unsigned base = (unsigned)pos * 4u, rowb = (unsigned)n * 4u;
-    // row of frame f0 + j: rr - j, wrapping below 0 (FftProcessor.kt:226-227 writeIndex--)
-    // (frames past the chunk: an offset past num_records, which reads zeros without a memory
-    // access -- the loads stay unconditional, so the compiler counts them with vmcnt(N) instead
-    // of draining at every branch: conditional loads cost 50 vmcnt(0) waits, ~30 us a unit)
-    auto voff = [&](int j) {
-        return j < nf ? (int)(base + (unsigned)(j <= rr ? rr - j : rr - j + rows) * rowb) : (int)0x80000000u;
-    };
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    f4v x[IF];
-#pragma unroll
-    for (int j = 0; j < IF; j++) x[j] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff(j), 0, kSc1));
-    float pk[4], emi[4], b[4];
-    bool restart[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) pk[q] = emi[q] = -INFINITY, b[q] = 0.0f, restart[q] = false;
-    float am = 1.0f;
-    const float al = k->st_alpha, keep = 1.0f - al;
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-        const f4v v = x[j % IF];
-        if (j + IF < 32)  // refill the slot: IF frames stay in flight
-            x[j % IF] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, voff(j + IF), 0, kSc1));
-        if (j < nf) {
-            state_step(pk[0], emi[0], b[0], restart[0], v.x, al);
-            state_step(pk[1], emi[1], b[1], restart[1], v.y, al);
-            state_step(pk[2], emi[2], b[2], restart[2], v.z, al);
-            state_step(pk[3], emi[3], b[3], restart[3], v.w, al);
-            am *= keep;
-        }
-    }
-    const rsrc_t ps = make_rsrc(k->st_part + (size_t)c * n, n * 16);
-#pragma unroll
-    for (int q = 0; q < 4; q++)
-        buf_store_f32x4(pk[q], restart[q] ? -1.0f : am, b[q], emi[q], ps, (pos + q) * 16, 0);
-    if ((threadIdx.x & 1023) == 0) k->st_done[t] = k->st_gen;
-}
-#endif
-
 // DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
 // 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
 // STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
@@ -675,116 +604,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
     int pending_st = 0;
 
-    // ---- in-grid peak / EMA state (FftLaunch st_*; 64 K staged kernels).
-    // A work item's ring stores are write-through (sc1); once every wave has drained them
-    // (vmcnt(0) before a workgroup barrier) one lane adds 1 to st_cnt[chunk of the frame]
-    // (agent scope).  Between items the workgroup takes a unit (chunk c, kStRange storage
-    // positions) of a COMPLETE chunk: the lane that saw the count polled it, the others pass a
-    // barrier after it, and every row load is an sc1 load (MI355X_MICROARCH.md, valid
-    // hand-off forms, row 1).  Nothing ever waits for another workgroup without a bound, so
-    // the grid cannot deadlock however many workgroups are resident; units nobody took are
-    // computed by state_fused_kernel (fft_kernels.hip), which also folds every summary.
-    // Compiled only into builds with -DRFA_IGS=1 (round-5 A/B: profiles/r05/igs_*).
-    constexpr bool IGS = RFA_IGS && STG && RS == 2 && LOGM == 15 && !COMPLEX_OUT && (DIAG & ~32) == 0;
-    // the st_* arguments are read through an opaque kernarg pointer where they are used, so
-    // hipcc cannot hoist them into registers held across the FFT (they pushed its SGPR spills
-    // 16 -> 104 and cost a VGPR spill when held)
-    // (readfirstlane: an inline-asm result counts as divergent, and descriptors built from
-    // divergent values would land in VGPRs where the store asm wants SGPRs)
-    using KArg = const __attribute__((address_space(4))) FftLaunch;
-    auto st_args = [] {
-        const unsigned long long p = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
-        unsigned lo = (unsigned)p, hi = (unsigned)(p >> 32);
-        asm volatile("" : "+s"(lo), "+s"(hi));
-        lo = __builtin_amdgcn_readfirstlane(lo);
-        hi = __builtin_amdgcn_readfirstlane(hi);
-        return (KArg *)(((unsigned long long)hi << 32) | lo);
-    };
-    // re-read per use through the opaque pointer: a loop-invariant flag would let hipcc
-    // unswitch the item loop into two copies of the whole FFT (twice the code, 5x the spills)
-    auto igs_on = [&] {
-        if constexpr (!IGS) return false;
-        KArg *k = st_args();
-        return k->st_chunk_len > 0 && k->ring != nullptr && k->rows == nullptr;
-    };
-    int prev_chunk = -1;  // chunk of the previous item while its completion is not yet signalled
-#ifdef RFA_IGS_DEBUG
-    if constexpr (IGS) {
-        if (threadIdx.x == 0 && a.st_cnt) {
-            __hip_atomic_fetch_add(&a.st_cnt[kStDbg + 6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (igs_on()) __hip_atomic_fetch_add(&a.st_cnt[kStDbg + 7], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-#endif
-    auto st_signal = [&] {  // after every wave's vmcnt(0) and a barrier
-        if (threadIdx.x == 0) {
-            __hip_atomic_fetch_add(&st_args()->st_cnt[prev_chunk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#ifdef RFA_IGS_DEBUG
-            __hip_atomic_fetch_add(&st_args()->st_cnt[kStDbg + 2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-        }
-        prev_chunk = -1;
-    };
-    auto run_unit = [&](int t) {
-#if RFA_IGS
-        const unsigned long long kp = (unsigned long long)__builtin_amdgcn_kernarg_segment_ptr();
-        st_unit((unsigned)kp, (unsigned)(kp >> 32), t);
-#endif
-        (void)t;
-        pending_st = 0;  // the unit waited for its loads, so everything older (the staged frame) landed too
-    };
-    // thread 0's first chunk not known to be exhausted (its tickets all taken)
-    int st_floor = 0;
-    auto take_units = [&](int max_units) {
-        constexpr int ranges = M * RS / kStRange;
-        int *lds_slot = reinterpret_cast<int *>(lds + G::TW_LDS + G::SLOTS * G::HALFP);
-        for (int it = 0; max_units < 0 || it < max_units; it++) {
-            if (threadIdx.x == 0) {
-                KArg *k = st_args();
-                const int cl = k->st_chunk_len, nfr = k->n_frames, nch = (nfr + cl - 1) / cl;
-                unsigned *cnt = k->st_cnt, *tickets = cnt + kStMaxChunks;
-                const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + kStWaitTicks;
-                int unit = -1;  // -1: none (stop), >= 0: run it
-                // per-chunk tickets: a fetch-add on chunk c's counter either returns one of its
-                // units or says the chunk is exhausted -- no unit is lost and nobody retries.
-                // (One shared ticket lost ~150 of 256 units a call to a stale ready check; a
-                // compare-exchange on it serialised the grid on its retries: 8000 per call, 520 us.)
-                for (;;) {
-                    bool pending = false;
-                    for (int c = st_floor; c < nch; c++) {
-                        if (__hip_atomic_load(&tickets[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)ranges) {
-                            st_floor = c + 1;
-                            continue;
-                        }
-                        const unsigned need = 2u * (unsigned)min(nfr - c * cl, cl);  // RS = 2 items per frame
-                        if (__hip_atomic_load(&cnt[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-                            pending = true;  // chunks complete about in order: stop at the first open one
-                            break;
-                        }
-                        const unsigned m = __hip_atomic_fetch_add(&tickets[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        if (m < (unsigned)ranges) {
-                            unit = c * ranges + (int)m;
-                            break;
-                        }
-                        st_floor = c + 1;
-#ifdef RFA_IGS_DEBUG
-                        __hip_atomic_fetch_add(&cnt[kStDbg + 4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-                    }
-                    if (unit >= 0 || !pending || max_units >= 0 || __builtin_amdgcn_s_memrealtime() >= t_end) break;
-                    __builtin_amdgcn_s_sleep(16);
-                }
-#ifdef RFA_IGS_DEBUG
-                __hip_atomic_fetch_add(&cnt[kStDbg + (unit >= 0 ? 3 : 5)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-                lds_slot[it & 1] = unit;
-            }
-            lds_barrier();
-            const int unit = __builtin_amdgcn_readfirstlane(lds_slot[it & 1]);  // uniform: descriptors in SGPRs
-            if (unit == -1) break;
-            run_unit(unit);
-        }
-    };
     auto body = [&](int u, int unext) {
         stamp(u, 0);
         // the lane index, opaque per item: the per-thread LDS bases derived from it are then
@@ -878,13 +697,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             if constexpr (!(DIAG & 4)) dftw<32, W8>(&v[b * 32]);
         stamp(u, 2);
         if constexpr (STG) {
-            if constexpr (IGS) {  // in-grid state: the previous item's ring stores, drained in every wave
-                if (prev_chunk >= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
             lds_barrier();  // every wave has read the staged frame before exchange 0 reuses the buffer
-            if constexpr (IGS) {
-                if (prev_chunk >= 0) st_signal();
-            }
             stamp(u, 7);
             if constexpr (SPLIT) {  // region B is free until the next item: its half of the next frame now
                 const int fn = frame_of(unext);
@@ -915,9 +728,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
         }
 
         if (!active) return;
-        if constexpr (IGS) {  // this item's chunk, signalled once its ring stores have drained
-            if (frame >= a.ring_first && igs_on()) prev_chunk = frame / st_args()->st_chunk_len;
-        }
         // ---- epilogue: sub-bin i + t*M/16 (i = tid + TPF*b) is full bin kk = r + RS*(i + t*M/16)
         // (kernel B of the large-N pair: kk = s + S*(...) with the runtime S = dif_ss and
         // s = dif_r; the stride and frame length below are then uniform runtime values)
@@ -1066,20 +876,6 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     for (int u = u0; u < items; it_count++) {
         const int un = next_item(u);
         body(u, un);
-        if constexpr (IGS) {
-            if (igs_on()) {
-                // between items at most one unit, and only from a complete chunk; after the last
-                // item, drain and signal it, then keep taking units until none is left (one call
-                // site: one inlined copy of the unit code)
-                const bool last = un >= items;
-                if (last && prev_chunk >= 0) {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    lds_barrier();
-                    st_signal();
-                }
-                take_units(last ? RFA_IGS_TAIL : 1);
-            }
-        }
         u = un;
     }
 }
@@ -1088,9 +884,7 @@ template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = f
 static hipError_t launch_wide_one(const FftLaunch &a) {
     using G = WGeo<LOGM, PT>;
     auto kern = &fft_wide_kernel<LOGM, PT, RS, FMT, CO, DIAG, STG>;
-    constexpr bool igs_k = RFA_IGS && STG && RS == 2 && LOGM == 15 && !CO && (DIAG & ~32) == 0;
-    // + 16 B: the in-grid state's unit broadcast slot (IGS, A/B builds with -DRFA_IGS=1)
-    const size_t lds = (size_t)G::LDS_BYTES + (igs_k ? 16 : 0);
+    const size_t lds = (size_t)G::LDS_BYTES;
     if (!a.wide_tw) return hipErrorInvalidValue;
     if (RS == 2 && FMT <= 2 && (DIAG & 16) == 0 && !a.window_cw) return hipErrorInvalidValue;  // residue 1's table
     static bool attr = false;
@@ -1114,7 +908,7 @@ static hipError_t launch_wide_one(const FftLaunch &a) {
                                                              lds) != hipSuccess || occ < 1)
                 occ = 1;
         }
-        blocks = std::min(items, cus * occ);
+        blocks = std::min(items, (a.cus > 0 ? a.cus : cus) * occ);
 #ifdef RFA_AB_BUILD
         if (const char *g = std::getenv("RFA_WIDE_GRID")) blocks = std::min(blocks, std::max(16, std::atoi(g)));  // A/B only
 #endif
