@@ -77,6 +77,9 @@ def parse(argv=None):
     p.add_argument("--ema-alpha", type=float, default=0.1)
     p.add_argument("--no-peak", action="store_true")
     p.add_argument("--ring-rows", type=int, default=500)
+    p.add_argument("--state-cus", type=int, default=0,
+                   help="streams mode: rfa_set_pipelined -- the peak / EMA pass on this many reserved CUs "
+                        "under the next call's FFT (0 = serial on the handle stream)")
     p.add_argument("--gather", action="store_true", help="shard mode: gather every call's rows to rank 0")
     p.add_argument("--batches-per-call", type=int, default=64,
                    help="shard mode: batches per rfa_process_batches call (1 = one launch per batch)")
@@ -227,7 +230,14 @@ def run_streams(args, ranks, fmt, steps, warmup, seed):
     eng = rfanalyzer_amd.SpectrumEngine(n, args.window, fmt, avg=args.avg, avg_length=min(30, args.ring_rows - 1),
                                         ema_alpha=args.ema_alpha, peak_hold=not args.no_peak,
                                         ring_rows=args.ring_rows, device=ranks.local)
+    if args.state_cus:
+        # pipelined state: a non-blocking stream (work on the HIP null stream would wait for the
+        # CU-masked streams, which are blocking streams); the timed region still ends with a
+        # device-wide synchronize, so every call's state pass is inside it
+        stream = torch.cuda.Stream(ranks.device)
     eng.set_stream(stream.cuda_stream)
+    if args.state_cus:
+        eng.set_pipelined(args.state_cus)
     pool = make_pool(torch, n, frames, fmt, args.pool_mib, seed, ranks.device)
     eng.set_tuning(100_000_000, 20_000_000)
     ctr = [0]

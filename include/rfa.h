@@ -119,6 +119,25 @@ RFA_API int rfa_use_own_stream(rfa_handle *h);
 RFA_API int rfa_get_stream(const rfa_handle *h, void **stream);
 RFA_API int rfa_synchronize(rfa_handle *h);
 
+/* Pipelined state (opt-in, no reference counterpart: FftProcessor.kt:135-245 runs the FFT,
+ * the ring write and the peak-hold one after another on one thread).  state_cus > 0 reserves
+ * that many CUs (a multiple of the device's XCD count, spread one per shader engine) for a
+ * CU-masked state stream that runs each call's peak / EMA / channel-mean pass, while the
+ * FFT kernels run on two CU-masked streams over the other CUs, alternating per call.  Call
+ * k's state pass then runs under call k + 1's FFT: a call that rewrites the whole ring
+ * (n_frames == ring_rows) writes the second ring buffer (the ring and its shift buffer swap
+ * per call, so rfa_get_state_generation advances), a call of at most ring_rows / 2 frames
+ * writes rows call k's pass does not read, and any other call waits for the previous pass.
+ * Pipelined calls are those with rows == NULL, a ring holding the batch, and peak-hold or
+ * EMA on; the rest run as before.
+ * The handle stream is NOT ordered after a pipelined call: rfa_join(h) enqueues on it a wait
+ * for every pipelined kernel so far (the input buffers may be reused and the ring / peaks /
+ * EMA read on that stream after it); rfa_synchronize and every other entry point join first.
+ * state_cus = 0 turns the mode off (after a join).  RFA_ERR_UNSUPPORTED when the device does
+ * not take CU masks or state_cus leaves no CUs for the FFT. */
+RFA_API int rfa_set_pipelined(rfa_handle *h, int32_t state_cus);
+RFA_API int rfa_join(rfa_handle *h);
+
 /* Batch processing.  `in` holds n_frames frames of N samples in the configured
  * format, frame f starting at byte f*frame_stride_bytes (0 = densely packed).
  * For a headerless file replayed in packets of P bytes with N <= P/bps, the

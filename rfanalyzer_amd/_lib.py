@@ -90,6 +90,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rfa_get_stream": (ctypes.c_int, [_h, ctypes.POINTER(_vp)]),
         "rfa_use_own_stream": (ctypes.c_int, [_h]),
         "rfa_synchronize": (ctypes.c_int, [_h]),
+        "rfa_set_pipelined": (ctypes.c_int, [_h, ctypes.c_int32]),
+        "rfa_join": (ctypes.c_int, [_h]),
         "rfa_process": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_process_host": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, _vp]),
         "rfa_process_batches": (ctypes.c_int, [_h, _vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,

@@ -69,6 +69,20 @@ struct rfa_handle {
     float4 *d_state_part = nullptr;   // chunked state update: [state_chunks][n]
     int state_chunks = 1;
     int state_fused = 1;              // single-launch chunked scan (A/B builds: RFA_STATE_FUSED=0 two kernels)
+    // pipelined state (rfa_set_pipelined): the state pass on a CU-masked stream,
+    // the FFT kernels on two CU-masked streams over the other CUs (alternating per call), so call
+    // k's pass runs under call k + 1's FFT
+    int pipe_cus = 0;                       // CUs of the state stream (0: off)
+    int pipe_fft_cus = 0;                   // CUs of the FFT streams (their persistent grids)
+    hipStream_t pipe_fft[2] = {nullptr, nullptr};
+    hipStream_t pipe_state = nullptr;
+    hipEvent_t pipe_in = nullptr;           // handle stream -> FFT stream: the call's input is ready
+    hipEvent_t pipe_fft_done[2] = {nullptr, nullptr};    // by call parity
+    hipEvent_t pipe_state_done[2] = {nullptr, nullptr};
+    bool pipe_recorded[2] = {false, false};
+    long long pipe_k = 0;                   // pipelined calls (parity: FFT stream and ring buffer)
+    int pipe_prev_frames = 0;               // frames of the last pipelined call while it is not joined
+    bool pipe_pending = false;              // pipelined work the handle stream is not ordered after
     float *d_boxcar = nullptr;
     bool have_tuning = false;
     // channel mean (FftProcessor.kt:143-157)
@@ -243,6 +257,7 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
         A.tw_d = h->d_dit_d;
         A.tw_cp = h->d_dit_cp;
         A.tw_dp = h->d_dit_dp;
+        A.pipe = h->dif_pipe;  // (the staging below is for the pipelined kernel only)
         if (A.pipe > 0 && A.fmt <= 1 && ((reinterpret_cast<uintptr_t>(A.in) | (uintptr_t)A.frame_stride) & 15) != 0) {
             // misaligned 8-bit frames: an aligned copy, so every 8-bit frame takes the same kernel
             // (and the same rounding) whatever the caller's pointer
@@ -257,7 +272,6 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
             A.frame_stride = (long long)fb;
         }
         A.z = h->d_dit_y;
-        A.pipe = h->dif_pipe;
         A.stream = a.stream;
         hipError_t e = rfa::launch_dif_front(A);
         if (e != hipSuccess) return e;
@@ -294,8 +308,8 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
     return hipSuccess;
 }
 
-int launch_main(rfa_handle *h, FftLaunch &a) {
-    a.stream = h->stream;
+int launch_main(rfa_handle *h, FftLaunch &a, hipStream_t st) {
+    a.stream = st;
     a.logn = h->logn;
     a.tw_coarse = h->d_twc;
     a.tw_fine = h->d_twf;
@@ -325,7 +339,7 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         if (h->ev_pending.size() > 4096) drain_events(h, true);
         e0 = get_event(h);
         e1 = get_event(h);
-        hipEventRecord(e0, h->stream);
+        hipEventRecord(e0, st);
     }
     hipError_t e = hipSuccess;
     if (h->logn > 17) {
@@ -349,20 +363,20 @@ int launch_main(rfa_handle *h, FftLaunch &a) {
         e = rfa::launch_fft(a);
     }
     if (h->profile) {
-        hipEventRecord(e1, h->stream);
+        hipEventRecord(e1, st);
         h->ev_pending.emplace_back(e0, e1);
     }
     if (e != hipSuccess) return hip_fail(h, e, "launch_fft");
     if (a.stamps) {  // profiling only: synchronous dump of this launch's phase stamps
-        std::vector<unsigned long long> st((size_t)kStampWords);
-        if (hipMemcpyAsync(st.data(), a.stamps, st.size() * 8, hipMemcpyDeviceToHost, h->stream) == hipSuccess &&
-            hipStreamSynchronize(h->stream) == hipSuccess) {
+        std::vector<unsigned long long> sv((size_t)kStampWords);
+        if (hipMemcpyAsync(sv.data(), a.stamps, sv.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess) {
             if (FILE *f = std::fopen(h->stamps_file.c_str(), "ab")) {
-                std::fwrite(st.data(), 8, st.size(), f);
+                std::fwrite(sv.data(), 8, sv.size(), f);
                 std::fclose(f);
             }
         }
-        hipMemsetAsync(a.stamps, 0, st.size() * 8, h->stream);
+        hipMemsetAsync(a.stamps, 0, sv.size() * 8, st);
     }
     return RFA_OK;
 }
@@ -378,6 +392,36 @@ int reset_peaks_ema(rfa_handle *h) {
     if (h->d_peaks) HIPCHK(h, rfa::launch_fill(h->d_peaks, h->n, kPeakFill, h->stream));
     if (h->d_ema) HIPCHK(h, rfa::launch_fill(h->d_ema, h->n, -INFINITY, h->stream));
     return RFA_OK;
+}
+
+// Order the handle stream after every pipelined kernel so far (rfa_join).  Every entry point
+// but a pipelined rfa_process joins first, so only pipelined calls overlap one another.
+int join(rfa_handle *h) {
+    if (!h->pipe_pending) return RFA_OK;
+    for (int p = 0; p < 2; p++) {
+        if (!h->pipe_recorded[p]) continue;
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->pipe_fft_done[p], 0));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->pipe_state_done[p], 0));
+    }
+    h->pipe_pending = false;
+    h->pipe_prev_frames = 0;
+    return RFA_OK;
+}
+
+void pipe_release(rfa_handle *h) {
+    for (hipStream_t *s : {&h->pipe_fft[0], &h->pipe_fft[1], &h->pipe_state}) {
+        if (*s) hipStreamSynchronize(*s), hipStreamDestroy(*s);
+        *s = nullptr;
+    }
+    for (hipEvent_t *e : {&h->pipe_in, &h->pipe_fft_done[0], &h->pipe_fft_done[1], &h->pipe_state_done[0],
+                          &h->pipe_state_done[1]}) {
+        if (*e) hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    h->pipe_recorded[0] = h->pipe_recorded[1] = false;
+    h->pipe_cus = h->pipe_fft_cus = 0;
+    h->pipe_pending = false;
+    h->pipe_prev_frames = 0;
 }
 
 }  // namespace
@@ -582,6 +626,7 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
 int rfa_destroy(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     hipSetDevice(h->device);
+    pipe_release(h);  // synchronises the pipelined streams
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
@@ -630,6 +675,7 @@ const char *rfa_last_error(const rfa_handle *h) { return h ? h->err.c_str() : "n
 int rfa_set_stream(rfa_handle *h, void *stream) {
     if (!h) return RFA_ERR_INVALID;
     if (int rc = set_device(h)) return rc;
+    if (int rc = join(h)) return rc;  // the old stream is ordered after the pipelined calls
     h->stream = (hipStream_t)stream;
     return RFA_OK;
 }
@@ -637,6 +683,7 @@ int rfa_set_stream(rfa_handle *h, void *stream) {
 int rfa_use_own_stream(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     if (int rc = set_device(h)) return rc;
+    if (int rc = join(h)) return rc;
     h->stream = h->own_stream;
     return RFA_OK;
 }
@@ -647,10 +694,55 @@ int rfa_get_stream(const rfa_handle *h, void **stream) {
     return RFA_OK;
 }
 
+int rfa_join(rfa_handle *h) {
+    if (!h) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    return join(h);
+}
+
+// CU masks (hipExtStreamCreateWithCUMask): the driver maps mask bit i to XCD i mod X, and its
+// index j = i / X within the XCD to shader engine j mod SE, CU slot j / SE -- so bits
+// [0, state_cus) put state_cus / X CUs on every XCD, each on another shader engine, and the
+// complement leaves every XCD the same number of FFT CUs (the FFT kernels' blocks b, b + 8, ...
+// share an XCD)
+int rfa_set_pipelined(rfa_handle *h, int32_t state_cus) {
+    if (!h || state_cus < 0) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    if ((rc = join(h))) return rc;
+    pipe_release(h);
+    if (state_cus == 0) return RFA_OK;
+    int ncu = 0, nxcc = 1;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || ncu <= 0)
+        return fail(h, RFA_ERR_HIP, "CU count");
+    if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, h->device) != hipSuccess || nxcc <= 0) nxcc = 1;
+    if (state_cus % nxcc || state_cus >= ncu)
+        return fail(h, RFA_ERR_UNSUPPORTED, "state_cus must be a multiple of the XCD count, below the CU count");
+    const int words = (ncu + 31) / 32;
+    std::vector<uint32_t> ms(words, 0u), mf(words, 0u);
+    for (int i = 0; i < ncu; i++) (i < state_cus ? ms : mf)[i / 32] |= 1u << (i % 32);
+    auto bail = [&](const char *what) {
+        pipe_release(h);
+        return fail(h, RFA_ERR_UNSUPPORTED, what);
+    };
+    if (hipExtStreamCreateWithCUMask(&h->pipe_state, (uint32_t)words, ms.data()) != hipSuccess)
+        return bail("CU-masked state stream");
+    for (hipStream_t &fs : h->pipe_fft)
+        if (hipExtStreamCreateWithCUMask(&fs, (uint32_t)words, mf.data()) != hipSuccess) return bail("CU-masked FFT stream");
+    for (hipEvent_t *e : {&h->pipe_in, &h->pipe_fft_done[0], &h->pipe_fft_done[1], &h->pipe_state_done[0],
+                          &h->pipe_state_done[1]})
+        if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail("pipeline events");
+    h->pipe_cus = state_cus;
+    h->pipe_fft_cus = ncu - state_cus;
+    return RFA_OK;
+}
+
 int rfa_synchronize(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
 }
@@ -661,6 +753,7 @@ static int apply_ring_resize(rfa_handle *h) {
     const int rn = h->pending_ring_rows;
     h->pending_ring_rows = -1;
     if (rn < 0 || rn == h->ring_rows) return RFA_OK;
+    if (int rc = join(h)) return rc;
     const size_t bytes = (size_t)rn * h->n * sizeof(float);
     float *nr = nullptr, *nt = nullptr;
     if (hipMalloc(&nr, bytes) != hipSuccess) return fail(h, RFA_ERR_NOMEM, "ring resize");
@@ -733,6 +826,34 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             state_rows = h->d_rows;
         }
     }
+    // pipelined state (rfa_set_pipelined): this call's FFT may start while the
+    // previous pipelined call's state pass still reads that call's rows, so it writes the ring's
+    // second buffer (the call rewrites every ring row) or only rows the previous call did not
+    // write; anything else first joins
+    const bool flip = (long long)n_frames == (long long)h->ring_rows;
+    const bool pipe = h->pipe_cus > 0 && need_state && rows_in_ring &&
+                      (flip || (long long)n_frames + h->pipe_prev_frames <= (long long)h->ring_rows);
+    if (!pipe) {
+        int rc = join(h);
+        if (rc) return rc;
+    }
+    const int par = (int)(h->pipe_k & 1);
+    hipStream_t fft_stream = h->stream, state_stream = h->stream;
+    if (pipe) {
+        // (N > 128 K: the decimation-in-frequency pair shares the handle's scratch z between its
+        // two kernels, so consecutive calls stay on one FFT stream)
+        fft_stream = h->pipe_fft[h->logn > 17 ? 0 : par];
+        state_stream = h->pipe_state;
+        // the input (and everything before it) is on the handle stream; the pass of call k - 2
+        // (same parity) read the buffer / rows this call writes
+        HIPCHK(h, hipEventRecord(h->pipe_in, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(fft_stream, h->pipe_in, 0));
+        if (h->pipe_recorded[par]) HIPCHK(h, hipStreamWaitEvent(fft_stream, h->pipe_state_done[par], 0));
+        if (flip) {  // the other ring buffer: its rows are all rewritten by this call
+            std::swap(h->d_ring, h->d_ring_tmp);
+            h->generation++;
+        }
+    }
     FftLaunch a;
     a.in = (const uint8_t *)in;
     a.frame_stride = (long long)stride;
@@ -740,6 +861,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
     a.fmt = fmt;
     a.window = window;
     a.rows = state_rows;
+    if (pipe) a.cus = h->pipe_fft_cus;
     if (h->d_ring) {
         a.ring = h->d_ring;
         a.ring_rows = h->ring_rows;
@@ -747,8 +869,12 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         a.ring_first = (int)std::max<long long>(0, (long long)n_frames - h->ring_rows);
         a.ring_logrs = h->ring_logrs;
     }
-    int rc = launch_main(h, a);
+    int rc = launch_main(h, a, fft_stream);
     if (rc) return rc;
+    if (pipe) {
+        HIPCHK(h, hipEventRecord(h->pipe_fft_done[par], fft_stream));
+        HIPCHK(h, hipStreamWaitEvent(state_stream, h->pipe_fft_done[par], 0));
+    }
     if (need_state || need_chan) {
         rfa::StateLaunch s;
         s.n = n;
@@ -759,7 +885,7 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
         s.part = h->d_state_part;
         s.max_chunks = h->state_chunks;
         s.fused = h->state_fused;
-        s.stream = h->stream;
+        s.stream = state_stream;
         if (rows_in_ring) {
             s.rows = h->d_ring;
             s.ring_rows = h->ring_rows;
@@ -774,12 +900,21 @@ static int process_impl(rfa_handle *h, const void *in, size_t n_frames, size_t s
             // means, then (channels wider than 16384 bins) the per-span partial sums
             const int spans = rfa::channel_mean_spans(chan_last - chan_first);
             const size_t words = n_frames * (size_t)(spans > 1 ? 1 + spans : 1);
+            if (pipe && words * sizeof(float) > h->d_chan_cap)  // the last pass may still write the old buffer
+                HIPCHK(h, hipStreamSynchronize(state_stream));
             int rc = ensure_device_buffer(h, (void **)&h->d_chan, &h->d_chan_cap, words * sizeof(float));
             if (rc) return rc;
             HIPCHK(h, rfa::launch_channel_mean(s, chan_first, chan_last, h->d_chan,
                                                spans > 1 ? h->d_chan + n_frames : nullptr));
             h->chan_count = n_frames;
         }
+    }
+    if (pipe) {
+        HIPCHK(h, hipEventRecord(h->pipe_state_done[par], state_stream));
+        h->pipe_recorded[par] = true;
+        h->pipe_pending = true;
+        h->pipe_prev_frames = (int)n_frames;
+        h->pipe_k++;
     }
     if (h->d_ring) {
         const long long R = h->ring_rows;
@@ -848,6 +983,7 @@ int rfa_process_host(rfa_handle *h, const void *in, size_t n_frames, size_t fram
     }
     rc = process_impl(h, h->d_in, n_frames, stride, d_rows, h->d_window, h->cfg.input_format);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;  // synchronous: the next call's copy reuses d_in
     if (rows)
         HIPCHK(h, hipMemcpyAsync(rows, d_rows, n_frames * (size_t)h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -898,6 +1034,7 @@ int rfa_set_tuning(rfa_handle *h, int64_t frequency, int64_t sample_rate) {
     if (!h || sample_rate <= 0) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     if (!h->have_tuning) {
         h->have_tuning = true;
         h->last_frequency = frequency;
@@ -949,6 +1086,7 @@ int rfa_draw_preprocess(rfa_handle *h, const rfa_draw_params *p, uint32_t *color
     if (peaks_y && !h->d_peaks) return fail(h, RFA_ERR_STATE, "peak-hold y needs peak_hold");
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     const int n = h->n, R = h->ring_rows, W = p->width, L = p->average_length;
     // AnalyzerSurface.kt:650-672, in the reference's types (Long, Double, Float, Int)
     const float samples_per_hz = (float)n / (float)h->last_sample_rate;
@@ -1048,6 +1186,7 @@ int rfa_row_window_stats(rfa_handle *h, const int32_t *lo, const int32_t *hi, si
     if (count == 0) return RFA_OK;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     const size_t b = (count * 4 + 255) & ~(size_t)255;
     rc = ensure_device_buffer(h, &h->d_draw, &h->d_draw_cap, 4 * b);
     if (rc) return rc;
@@ -1076,6 +1215,7 @@ int rfa_get_channel_means(rfa_handle *h, float *out, size_t capacity, size_t *co
     if (!h || !count || (!out && capacity)) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     const size_t k = std::min(capacity, h->chan_count);
     if (k) HIPCHK(h, hipMemcpyAsync(out, h->d_chan + h->chan_offset, k * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1088,6 +1228,7 @@ int rfa_get_peaks(rfa_handle *h, float *out) {
     if (!h->d_peaks) return fail(h, RFA_ERR_STATE, "peak_hold disabled");
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     HIPCHK(h, hipMemcpyAsync(out, h->d_peaks, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
@@ -1098,6 +1239,7 @@ int rfa_get_ema(rfa_handle *h, float *out) {
     if (!h->d_ema) return fail(h, RFA_ERR_STATE, "EMA disabled");
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     HIPCHK(h, hipMemcpyAsync(out, h->d_ema, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return RFA_OK;
@@ -1109,6 +1251,7 @@ int rfa_get_boxcar(rfa_handle *h, int32_t length, float *out) {
     if (length >= h->ring_rows) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     HIPCHK(h, rfa::launch_boxcar(h->d_ring, h->ring_rows, h->n, h->ring_logrs, h->read_index, length, h->d_boxcar,
                                   h->stream));
     HIPCHK(h, hipMemcpyAsync(out, h->d_boxcar, h->n * sizeof(float), hipMemcpyDeviceToHost, h->stream));
@@ -1121,6 +1264,7 @@ int rfa_get_ring(rfa_handle *h, float *out, int32_t *read_index, int32_t *write_
     if (!h->d_ring) return fail(h, RFA_ERR_STATE, "ring disabled");
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     if (out) {
         const float *src = h->d_ring;
         if (h->ring_logrs) {  // residue-major storage -> natural rows (d_ring_tmp is free outside a retune)
@@ -1140,6 +1284,7 @@ int rfa_reset_state(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     h->write_index = h->read_index = 0;
     h->have_rows = false;
     h->have_tuning = false;
@@ -1165,6 +1310,7 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
     if (fft_size == h->n) return RFA_OK;
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     rfa_config c = h->cfg;
     c.fft_size = fft_size;
@@ -1183,8 +1329,10 @@ int rfa_set_fft_size(rfa_handle *h, int32_t fft_size) {
     if (h->stream != h->own_stream) nh->stream = h->stream;
     nh->profile = h->profile;
     nh->generation = h->generation + 1;
+    const int pipe_cus = h->pipe_cus;
     std::swap(*h, *nh);
     rfa_destroy(nh);  // the old tables and buffers
+    if (pipe_cus) return rfa_set_pipelined(h, pipe_cus);
     return RFA_OK;
 }
 
@@ -1210,6 +1358,9 @@ int rfa_get_ring_positions(const rfa_handle *h, int32_t *positions, size_t count
 
 int rfa_get_device_state(rfa_handle *h, float **ring, float **peaks, float **ema) {
     if (!h) return RFA_ERR_INVALID;
+    int rc = set_device(h);
+    if (rc) return rc;
+    if ((rc = join(h))) return rc;  // device readers on the handle stream see the last call's state
     if (ring) *ring = h->d_ring;
     if (peaks) *peaks = h->d_peaks;
     if (ema) *ema = h->d_ema;
@@ -1221,6 +1372,7 @@ static int single_frame(rfa_handle *h, const void *host_in, size_t in_bytes, int
                         float *host_db, float2 *host_cplx) {
     int rc = set_device(h);
     if (rc) return rc;
+    if ((rc = join(h))) return rc;
     const size_t n = (size_t)h->n;
     const size_t out_bytes = host_cplx ? n * sizeof(float2) : n * sizeof(float);
     rc = ensure_device_buffer(h, &h->d_in, &h->d_in_cap, in_bytes);
@@ -1236,7 +1388,7 @@ static int single_frame(rfa_handle *h, const void *host_in, size_t in_bytes, int
     a.window = d_window;
     if (host_cplx) a.complex_out = (float2 *)h->d_rows;
     else a.rows = h->d_rows;
-    rc = launch_main(h, a);
+    rc = launch_main(h, a, h->stream);
     if (rc) return rc;
     HIPCHK(h, hipMemcpyAsync(host_cplx ? (void *)host_cplx : (void *)host_db, h->d_rows, out_bytes,
                              hipMemcpyDeviceToHost, h->stream));

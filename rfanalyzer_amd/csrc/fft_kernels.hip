@@ -554,6 +554,9 @@ __global__ void state_combine_kernel(StateLaunch a, int chunks) {
 #ifndef RFA_STATE_UNROLL
 #define RFA_STATE_UNROLL 4
 #endif
+#ifndef RFA_STATE_LOAD_AUX
+#define RFA_STATE_LOAD_AUX 0  // cache policy of the ring-row loads (A/B: 2 = nt)
+#endif
 template <int CH>
 __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chunk_len) {
     constexpr int TPC = 256 / CH, BPB = 4 * TPC;  // threads per chunk, bins per block
@@ -584,7 +587,7 @@ __global__ void __launch_bounds__(256) state_fused_kernel(StateLaunch a, int chu
             if (rr < 0) rr += a.ring_rows;
 #pragma unroll RFA_STATE_UNROLL
             for (int f = f0; f < f1; f++) {
-                step(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((unsigned)rr * rowb + (unsigned)bin * 4u), 0, 0)));
+                step(__builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((unsigned)rr * rowb + (unsigned)bin * 4u), 0, RFA_STATE_LOAD_AUX)));
                 rr = rr == 0 ? a.ring_rows - 1 : rr - 1;
             }
         } else {

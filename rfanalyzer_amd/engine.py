@@ -160,6 +160,16 @@ class SpectrumEngine:
     def synchronize(self) -> None:
         self._check(_lib.lib().rfa_synchronize(self._h), "rfa_synchronize")
 
+    def set_pipelined(self, state_cus: int) -> None:
+        """rfa_set_pipelined: the peak / EMA pass of call k on `state_cus` reserved CUs under
+        call k + 1's FFT (0: off).  The handle stream is then ordered after a call only by
+        join() (or synchronize() / any other entry point)."""
+        self._check(_lib.lib().rfa_set_pipelined(self._h, int(state_cus)), "rfa_set_pipelined")
+
+    def join(self) -> None:
+        """rfa_join: order the handle stream after every pipelined call so far."""
+        self._check(_lib.lib().rfa_join(self._h), "rfa_join")
+
     # -- FftProcessor state -----------------------------------------------------
     def set_tuning(self, frequency: int, sample_rate: int) -> None:
         self._check(_lib.lib().rfa_set_tuning(self._h, int(frequency), int(sample_rate)), "rfa_set_tuning")

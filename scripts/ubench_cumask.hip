@@ -33,6 +33,46 @@ __global__ void census(unsigned *out) {
     }
 }
 
+// every block records its (XCC, HW_ID) after a ~20 us spin, so a block per resident slot is seen
+__global__ void census2(unsigned *out) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < 2000) __builtin_amdgcn_s_sleep(4);
+    if (threadIdx.x == 0) {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        out[2 * blockIdx.x] = hw;
+        out[2 * blockIdx.x + 1] = xcc;
+    }
+}
+
+static void census_mask(const char *name, const std::vector<uint32_t> &m, int words) {
+    hipStream_t s;
+    CK(hipExtStreamCreateWithCUMask(&s, words, m.data()));
+    std::vector<uint32_t> got(words, 0u);
+    CK(hipExtStreamGetCUMask(s, words, got.data()));
+    const int blocks = 2048;
+    unsigned *d;
+    CK(hipMalloc(&d, blocks * 8));
+    hipLaunchKernelGGL(census2, dim3(blocks), dim3(64), 0, s, d);
+    CK(hipStreamSynchronize(s));
+    std::vector<unsigned> h(2 * blocks);
+    CK(hipMemcpy(h.data(), d, h.size() * 4, hipMemcpyDeviceToHost));
+    std::map<unsigned, int> cus;       // (xcc, se, sh, cu) -> blocks
+    std::map<unsigned, int> per_xcc;   // xcc -> distinct CUs
+    for (int b = 0; b < blocks; b++) {
+        const unsigned hw = h[2 * b], xcc = h[2 * b + 1] & 0xf;
+        cus[(xcc << 16) | (((hw >> 13) & 7) << 8) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)]++;
+    }
+    for (auto &kv : cus) per_xcc[kv.first >> 16]++;
+    std::printf("mask %-12s set bits %3d (readback word0 %08x): %zu distinct CUs; per XCC:", name,
+                [&] { int c = 0; for (uint32_t w : m) c += __builtin_popcount(w); return c; }(), got[0], cus.size());
+    for (auto &kv : per_xcc) std::printf(" x%u:%d", kv.first, kv.second);
+    std::printf("\n");
+    CK(hipFree(d));
+    CK(hipStreamDestroy(s));
+}
+
 __global__ void fill(float4 *p, size_t n, float v) {
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         p[i] = make_float4(v, v + 1.f, v, v);
@@ -69,6 +109,25 @@ int main() {
     unsigned *d_out;
     CK(hipMalloc(&d_out, 64 * 2 * 4));
     const int words = (ncu + 31) / 32;
+    // ---- 0. census by mask (all blocks' CUs)
+    {
+        auto range = [&](int lo, int hi) {
+            std::vector<uint32_t> m(words, 0u);
+            for (int b = lo; b < hi; b++) m[b / 32] |= 1u << (b % 32);
+            return m;
+        };
+        census_mask("all", range(0, ncu), words);
+        census_mask("{0}", range(0, 1), words);
+        census_mask("{1}", range(1, 2), words);
+        census_mask("[0,8)", range(0, 8), words);
+        census_mask("[8,16)", range(8, 16), words);
+        census_mask("[0,16)", range(0, 16), words);
+        census_mask("[0,32)", range(0, 32), words);
+        census_mask("[16,256)", range(16, ncu), words);
+        census_mask("[24,256)", range(24, ncu), words);
+        census_mask("[32,64)", range(32, 64), words);
+    }
+    if (std::getenv("CENSUS_ONLY")) return 0;
     // ---- 1. census
     std::map<int, std::vector<int>> xcc_bits;  // xcc -> bits
     std::vector<int> bit_xcc(ncu, -1);
@@ -76,7 +135,7 @@ int main() {
         std::vector<uint32_t> m(words, 0u);
         m[b / 32] = 1u << (b % 32);
         hipStream_t s;
-        CK(hipExtStreamCreateWithCUMask(&s, words * 32, m.data()));
+        CK(hipExtStreamCreateWithCUMask(&s, words, m.data()));
         CK(hipMemset(d_out, 0xff, 64 * 2 * 4));
         hipLaunchKernelGGL(census, dim3(16), dim3(64), 0, s, d_out);
         CK(hipStreamSynchronize(s));
@@ -108,7 +167,7 @@ int main() {
         for (auto &kv : xcc_bits)
             for (int i = 0; i < k / nx && i < (int)kv.second.size(); i++) m[kv.second[i] / 32] |= 1u << (kv.second[i] % 32);
         hipStream_t s;
-        CK(hipExtStreamCreateWithCUMask(&s, words * 32, m.data()));
+        CK(hipExtStreamCreateWithCUMask(&s, words, m.data()));
         for (int chunks : {16, 32}) {
             const int chunk = (R + chunks - 1) / chunks;
             const int threads = chunks * (N / 4), grid = threads / 256;

@@ -53,6 +53,11 @@ DB_TOL_S16_EVERY_BIN = 0.05
 DB_TOL_BATCH_EVERY_BIN = 0.02      # the bar of the beyond-pffft's-error form, printed (round 3's bar)
 BATCH_EXCEED_SHARE = 1e-6
 DB_TOL_BATCH_MAX = 0.1
+# Config 2's Hann frames (cf32, tones 0.5 / 0.05, noise 0.01): the deep Hann bins sit ~45 dB under
+# the tone, where the reference's pffft itself is 0.08-0.65 dB from float64 on four captures
+# (DESIGN.md §4).  The worst bin there is a sanity bound only (a wrong twiddle or bin order moves
+# whole rows by dB); the comparative bars are the deep-bin error and the tail quantile.
+DB_TOL_HANN_DEEP_MAX = 1.0
 # The raw every-bin distance to the reference's pffft rows on that batch: at most
 # |librfa - float64| + |pffft - float64|, bar 0.15 dB (printed with its source).
 DB_TOL_RAW_PFFFT = 0.15
@@ -114,8 +119,8 @@ CURRENT_TEST = ""
 # bin is ~ eps * sqrt(c log2 N / N) of the row's total (Parseval) magnitude, i.e. 82 (N = 1 K)
 # to 90 dB (N = 64 K) under the row level in this unit (the reference's own pffft leaves its
 # rounding noise 88 dB under a pure tone, tests/golden kat_tone_bin_n16384_none, where the
-# float64 transform has -126 dB).  A bin counts as resolved only when BOTH sides are at least
-# RESOLVE_DB = 60 dB under the row level: >= 20 dB above that noise, so fp32 rounding is
+# float64 transform has -126 dB).  A bin counts as resolved only when BOTH sides are no more
+# than RESOLVE_DB = 60 dB below the row level: >= 20 dB above that noise, so fp32 rounding is
 # <= ~1 % of the bin there (round 4 used 80 dB, within 2-10 dB of the noise, and its summary
 # line compared noise with noise -- VERDICT r4).  The others are counted, never compared
 # (db_stats' structural check still wants them deep on both sides).  The session summary

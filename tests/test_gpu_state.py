@@ -496,3 +496,111 @@ def test_ring_positions_map_device_rows(rfa, n):
         e.synchronize()
         assert hip.hipMemcpy(ctypes.c_void_p(raw.ctypes.data), r, ctypes.c_size_t(raw.nbytes), 2) == 0
         np.testing.assert_array_equal(raw[:, pos], ring)
+
+
+# ---------------------------------------------------------------- pipelined state (rfa_set_pipelined)
+def _pipe_pair(rfa, n, ring_rows, state_cus, chan=None, **kw):
+    kw = dict(avg="ema", ema_alpha=0.1, peak_hold=True, ring_rows=ring_rows, **kw)
+    a, b = rfa.SpectrumEngine(n, "blackman", "s8", **kw), rfa.SpectrumEngine(n, "blackman", "s8", **kw)
+    for e in (a, b):
+        e.set_tuning(433_920_000, 20_000_000)
+        if chan:
+            e.set_channel(*chan)
+    b.set_pipelined(state_cus)
+    return a, b
+
+
+def _same_state(a, b, n_frames_last):
+    """Serial engine a and pipelined engine b hold bit-identical ring, peaks, EMA and channel
+    means (the same kernels on the same rows; only the streams and CU sets differ)."""
+    ra, ria, wia = a.ring()
+    rb, rib, wib = b.ring()
+    assert (ria, wia) == (rib, wib)
+    np.testing.assert_array_equal(ra, rb)
+    np.testing.assert_array_equal(a.peaks(), b.peaks())
+    np.testing.assert_array_equal(a.ema(), b.ema())
+    np.testing.assert_array_equal(a.channel_means(), b.channel_means())
+
+
+@pytest.mark.parametrize("n,ring_rows,batches", [
+    (65536, 500, (500, 500, 500, 500)),    # B = R: every call writes the other ring buffer
+    (65536, 500, (200, 250, 100, 40, 60)),  # B_k + B_k-1 <= R: rows the last call did not write
+    (65536, 500, (300, 300, 500, 137, 500)),  # neither: joins, then flips again
+    (8192, 64, (64, 64, 30, 30, 64, 1)),
+    (1048576, 32, (16, 16, 8, 16)),         # column-order ring, state_tile_kernel on the state stream
+])
+def test_pipelined_state_equals_serial(rfa, n, ring_rows, batches):
+    """rfa_set_pipelined (the peak / EMA pass of call k on reserved CUs under call k + 1's FFT,
+    DESIGN.md §5.3c): the same batches through a serial engine and a pipelined one give
+    bit-identical rings, peaks, EMA and channel means, read after the last call (the getters
+    join), and both match the oracle.  Device-resident input, several calls in flight."""
+    import torch
+    total = sum(batches)
+    data, rows = _cfg3_rows(n, total, 5)
+    dev = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    fb = 2 * n
+    a, b = _pipe_pair(rfa, n, ring_rows, 16, chan=(433_900_000, 433_990_000))
+    with a, b:
+        f = 0
+        g0 = b.state_generation()
+        for k, nb in enumerate(batches):
+            for e in (a, b):
+                e.process_device(dev.data_ptr() + f * fb, nb, 0, None)
+            f += nb
+        _same_state(a, b, batches[-1])
+        if all(x == ring_rows for x in batches):
+            assert b.state_generation() == g0 + len(batches)  # one ring swap per call
+        assert gu.db_diff(b.peaks(), rows[:total].max(0)) <= gu.DB_TOL
+        assert gu.db_diff(b.ema(), processor.ema_batch(rows[:total], 0.1)) <= gu.DB_TOL
+
+
+def test_pipelined_state_with_retune_resize_and_reads_between_calls(rfa):
+    """Every other entry point joins the pipeline first: a shifting retune, a ring resize, a
+    mid-stream peaks / ring read and rfa_get_device_state between pipelined calls leave the
+    pipelined engine bit-identical to the serial one."""
+    import ctypes
+    import torch
+    n, R = 65536, 100
+    data, rows = _cfg3_rows(n, 520, 7)
+    dev = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    torch.cuda.synchronize()
+    fb = 2 * n
+    a, b = _pipe_pair(rfa, n, R, 24)
+    with a, b:
+        f = 0
+        for k, nb in enumerate((100, 100, 40, 50, 100, 30, 100)):
+            for e in (a, b):
+                if k == 2:
+                    e.set_tuning(433_920_000 + 150_000, 20_000_000)  # shift by 491 bins
+                if k == 4:
+                    e.set_ring_rows(120)
+                e.process_device(dev.data_ptr() + f * fb, nb, 0, None)
+            f += nb
+            if k in (1, 3):
+                np.testing.assert_array_equal(a.peaks(), b.peaks())
+            if k == 5:
+                r, p, m = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+                assert rfa.lib().rfa_get_device_state(b.handle, ctypes.byref(r), ctypes.byref(p), ctypes.byref(m)) == 0
+                got = np.empty(n, np.float32)
+                hip = ctypes.CDLL("libamdhip64.so")
+                b.synchronize()
+                assert hip.hipMemcpy(ctypes.c_void_p(got.ctypes.data), m, ctypes.c_size_t(got.nbytes), 2) == 0
+                np.testing.assert_array_equal(got, a.ema())
+        _same_state(a, b, 100)
+
+
+def test_pipelined_state_arguments(rfa):
+    """state_cus must be a multiple of the XCD count and leave CUs for the FFT; 0 turns the
+    mode off (host getters keep working in either mode)."""
+    import torch
+    props = torch.cuda.get_device_properties(0)
+    with rfa.SpectrumEngine(1024, "blackman", "s8", peak_hold=True, ring_rows=8) as e:
+        for bad in (3, props.multi_processor_count):
+            with pytest.raises(RuntimeError):
+                e.set_pipelined(bad)
+        e.set_pipelined(8)
+        e.set_pipelined(0)
+        e.set_tuning(1_000_000, 100_000)
+        e.process(np.zeros(2 * 1024 * 8, np.int8).tobytes(), 8, rows=False)
+        assert np.all(np.isneginf(e.peaks()) | (e.peaks() < -100))
