@@ -48,6 +48,8 @@ struct rfa_handle {
     size_t d_dit_db_cap = 0;
     int dit_frames = 1;               // frames per kernel-A/B pair (scratch <= kDitScratch)
     int dif_pipe = 6;                 // frame groups of the pipelined front kernel (8-bit input)
+    hipStream_t dif_stream2 = nullptr;  // A/B builds (RFA_DIF_SPLIT): second stream of the split batch
+    hipEvent_t *dif_split_ev = nullptr; // [2]: first half's kernel A done, second half done
     int variant = 0;                  // 1: the narrow kernel (A/B builds: RFA_KERNEL=narrow)
     int stage = 1;                    // LDS-DMA staged input in the wide kernel (A/B builds: RFA_STAGE=0 off)
     // profiling / ablation hooks, set only by A/B builds (-DRFA_AB_BUILD, scripts/build_variant.sh);
@@ -271,39 +273,63 @@ static hipError_t launch_large(rfa_handle *h, const FftLaunch &a) {
             A.in = h->d_dit_in;
             A.frame_stride = (long long)fb;
         }
-        A.z = h->d_dit_y;
-        A.stream = a.stream;
-        hipError_t e = rfa::launch_dif_front(A);
-        if (e != hipSuccess) return e;
+        // one kernel pair over frames [g0, g0 + gc) of this batch on stream st (scratch z and the
+        // row scratch are frame-major, so disjoint frame ranges use disjoint scratch)
+        auto pair = [&](int g0, int gc, hipStream_t st) -> hipError_t {
+            rfa::DifLaunch Ah = A;
+            Ah.in = A.in + (size_t)g0 * (size_t)A.frame_stride;
+            Ah.n_frames = gc;
+            Ah.z = h->d_dit_y + (size_t)g0 * n;
+            Ah.stream = st;
+            hipError_t e = rfa::launch_dif_front(Ah);
+            if (e != hipSuccess) return e;
+            if (st == a.stream && h->dif_split_ev) {  // (A/B split: the second half's kernel A may start now)
+                e = hipEventRecord(h->dif_split_ev[0], st);
+                if (e != hipSuccess) return e;
+            }
 #ifdef RFA_DIT_FLUSH_MB
-        {  // A/B builds only: evict the scratch z from the Infinity Cache before kernel B
-            static void *flush = nullptr;
-            if (!flush && hipMalloc(&flush, (size_t)RFA_DIT_FLUSH_MB << 20) != hipSuccess) return hipErrorOutOfMemory;
-            e = hipMemsetAsync(flush, f0 & 0xff, (size_t)RFA_DIT_FLUSH_MB << 20, a.stream);
-            if (e != hipSuccess) return e;
-        }
+            {  // A/B builds only: evict the scratch z from the Infinity Cache before kernel B
+                static void *flush = nullptr;
+                if (!flush && hipMalloc(&flush, (size_t)RFA_DIT_FLUSH_MB << 20) != hipSuccess) return hipErrorOutOfMemory;
+                e = hipMemsetAsync(flush, f0 & 0xff, (size_t)RFA_DIT_FLUSH_MB << 20, st);
+                if (e != hipSuccess) return e;
+            }
 #endif
-        FftLaunch B = a;
-        B.in = reinterpret_cast<const uint8_t *>(h->d_dit_y);
-        B.frame_stride = (long long)n * (long long)sizeof(float2);
-        B.n_frames = cnt;
-        B.fmt = rfa::kFmtDif;
-        B.dif_ss = s;
-        B.window = nullptr;
-        B.window_il = nullptr;
-        B.rows = a.rows ? h->d_dit_db : nullptr;
-        B.complex_out = a.complex_out ? a.complex_out + (size_t)f0 * n : nullptr;
-        B.ring_base = a.ring_base - f0;  // frame f0 + f of the call is frame f of this pair
-        B.ring_first = a.ring_first - f0;
-        B.stage = h->stage;  // kernel B stages half of its next item's z_s (fft_wide.hip QSTB)
-        B.diag = 0;
-        B.stamps = nullptr;
-        e = rfa::launch_fft_wide(B);
-        if (e != hipSuccess) return e;
-        if (a.rows) {
-            e = rfa::launch_cols_to_rows(h->d_dit_db, a.rows + (size_t)f0 * n, cnt, h->logn, a.stream);
+            FftLaunch B = a;
+            B.stream = st;
+            B.in = reinterpret_cast<const uint8_t *>(h->d_dit_y + (size_t)g0 * n);
+            B.frame_stride = (long long)n * (long long)sizeof(float2);
+            B.n_frames = gc;
+            B.fmt = rfa::kFmtDif;
+            B.dif_ss = s;
+            B.window = nullptr;
+            B.window_il = nullptr;
+            B.rows = a.rows ? h->d_dit_db + (size_t)g0 * n : nullptr;
+            B.complex_out = a.complex_out ? a.complex_out + (size_t)(f0 + g0) * n : nullptr;
+            B.ring_base = a.ring_base - (f0 + g0);  // frame f0 + g0 + f of the call is frame f of this pair
+            B.ring_first = a.ring_first - (f0 + g0);
+            B.stage = h->stage;  // kernel B stages half of its next item's z_s (fft_wide.hip QSTB)
+            B.diag = 0;
+            B.stamps = nullptr;
+            e = rfa::launch_fft_wide(B);
             if (e != hipSuccess) return e;
+            if (a.rows) e = rfa::launch_cols_to_rows(h->d_dit_db + (size_t)g0 * n, a.rows + (size_t)(f0 + g0) * n, gc, h->logn, st);
+            return e;
+        };
+        hipError_t e = hipSuccess;
+        if (h->dif_split_ev && cnt >= 2) {
+            // A/B builds (RFA_DIF_SPLIT): the batch in two halves, the second on its own stream once
+            // the first half's kernel A is done, so its kernel A runs beside the first half's kernel B
+            const int h1 = cnt / 2;
+            e = pair(0, h1, a.stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(h->dif_stream2, h->dif_split_ev[0], 0);
+            if (e == hipSuccess) e = pair(h1, cnt - h1, h->dif_stream2);
+            if (e == hipSuccess) e = hipEventRecord(h->dif_split_ev[1], h->dif_stream2);
+            if (e == hipSuccess) e = hipStreamWaitEvent(a.stream, h->dif_split_ev[1], 0);
+        } else {
+            e = pair(0, cnt, a.stream);
         }
+        if (e != hipSuccess) return e;
     }
     return hipSuccess;
 }
@@ -569,6 +595,13 @@ int rfa_create(const rfa_config *cfg, rfa_handle **out) {
     if (const char *d = std::getenv("RFA_DIAG")) h->diag = std::atoi(d);
     if (const char *d = std::getenv("RFA_PHASE_NS")) h->phase_ticks = std::atoi(d) / 10;
     if (const char *d = std::getenv("RFA_DIF_PIPE")) h->dif_pipe = std::max(0, std::atoi(d));
+    if (const char *d = std::getenv("RFA_DIF_SPLIT"); d && std::atoi(d) && logn > 17) {
+        h->dif_split_ev = new hipEvent_t[2];
+        if (hipStreamCreateWithFlags(&h->dif_stream2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&h->dif_split_ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&h->dif_split_ev[1], hipEventDisableTiming) != hipSuccess)
+            return bail(RFA_ERR_HIP);
+    }
     if (const char *d = std::getenv("RFA_STAGE")) h->stage = std::atoi(d);
     if (const char *d = std::getenv("RFA_STAMPS_FILE")) {
         h->stamps_file = d;
@@ -627,6 +660,13 @@ int rfa_destroy(rfa_handle *h) {
     if (!h) return RFA_ERR_INVALID;
     hipSetDevice(h->device);
     pipe_release(h);  // synchronises the pipelined streams
+    if (h->dif_split_ev) {
+        hipStreamSynchronize(h->dif_stream2);
+        hipStreamDestroy(h->dif_stream2);
+        hipEventDestroy(h->dif_split_ev[0]);
+        hipEventDestroy(h->dif_split_ev[1]);
+        delete[] h->dif_split_ev;
+    }
     if (h->stream) hipStreamSynchronize(h->stream);
     for (auto &pr : h->ev_pending) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (auto e : h->ev_pool) hipEventDestroy(e);

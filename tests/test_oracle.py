@@ -42,6 +42,26 @@ def test_reference_pffft_ordered_vs_numpy(n):
     assert err < 1e-5
 
 
+@pytest.mark.skipif(not oracle.exact_available(), reason="exact-twiddle pffft build absent")
+@pytest.mark.parametrize("n", [1024, 48000, 65536, 1 << 20])
+def test_exact_twiddle_pffft_build(n):
+    """oracle/exact_twiddle.c (diagnostic): the reference's pffft with its two
+    twiddle tables recomputed from exact angles.  Every table entry moved by <= 1e-6 (the restated
+    setup layout is the reference's), the transform stays within 1e-6 of max |X| of the unmodified
+    pffft, and its RMS error against float64 is below pffft's (the float-argument twiddles of
+    pffft.c:1140,1156,1160-1161,1261 are a third of pffft's rounding error)."""
+    x = np.random.default_rng(n).standard_normal(2 * n).astype(np.float32)
+    a = oracle.ref_fft_ordered(x)
+    b = np.empty_like(x)
+    assert oracle.exact().exact_fft_ordered(oracle._f32ptr(x), n, oracle._f32ptr(b)) == 0
+    assert 0 < oracle.exact().exact_max_change() <= 1e-6
+    f = np.fft.fft(x[0::2].astype(np.float64) + 1j * x[1::2])
+    ca, cb = a[0::2] + 1j * a[1::2].astype(np.float64), b[0::2] + 1j * b[1::2].astype(np.float64)
+    m = np.abs(f).max()
+    assert np.abs(ca - cb).max() <= 1e-6 * m
+    assert np.sqrt(np.mean(np.abs(cb - f) ** 2)) < np.sqrt(np.mean(np.abs(ca - f) ** 2))
+
+
 def test_kat_values():
     n = 1024
     imp = oracle.spectrum_rows(signals.kat_bytes("impulse", n), oracle.IN_F32_INTERLEAVED, n, 1, None, None)[0]
