@@ -128,7 +128,11 @@ bool w64_format(int fmt);
 constexpr int kWidePT = 32;  // wide kernel: points per thread (32 and 64 measured)
 // sub-FFT size of the wide kernel: N itself up to 16 K, else 32 K (one
 // 32 K-point workgroup per CU) with N / 32 K residues
-inline int wide_logm(int logn) { return logn <= 14 ? logn : 15; }
+#ifndef RFA_RES16K
+#define RFA_RES16K 0  // A/B builds: N = 64 K as four 16 K residue items (two workgroups per CU) -- the
+                      // co-scheduled re-read cluster form of VERDICT r5 item 3 (profiles/r06/)
+#endif
+inline int wide_logm(int logn) { return logn <= 14 ? logn : (RFA_RES16K && logn == 16 ? 14 : 15); }
 std::vector<float2> wide_twiddles(int logn, int pt, int lm);
 hipError_t launch_fft_wide(const FftLaunch &a);
 // N = 64 K (dB rows / ring; not the complex-out seam): the wave-decoupled kernel, one

@@ -1061,6 +1061,9 @@ hipError_t launch_fft_wide(const FftLaunch &a) {
     case 14: return co ? wide_by_fmt<14, 32, 1, true>(a) : wide_by_fmt<14, 32, 1, false>(a);
     case 15: return co ? wide_by_fmt<15, 32, 1, true>(a) : wide_by_fmt<15, 32, 1, false>(a);
     case 16:
+#if RFA_RES16K
+        if (!co) return wide_by_fmt<14, 32, 4, false>(a);  // A/B: four 16 K residues per frame
+#endif
         if (co) return wide_by_fmt<15, 32, 2, true>(a);
         return w64_format(a.fmt) ? launch_fft64(a) : wide_by_fmt<15, 32, 2, false>(a);
     case 17: return co ? wide_by_fmt<15, 32, 4, true>(a) : wide_by_fmt<15, 32, 4, false>(a);
