@@ -766,15 +766,31 @@ int rfa_set_pipelined(rfa_handle *h, int32_t state_cus) {
         pipe_release(h);
         return fail(h, RFA_ERR_UNSUPPORTED, what);
     };
-    if (hipExtStreamCreateWithCUMask(&h->pipe_state, (uint32_t)words, ms.data()) != hipSuccess)
-        return bail("CU-masked state stream");
-    for (hipStream_t &fs : h->pipe_fft)
-        if (hipExtStreamCreateWithCUMask(&fs, (uint32_t)words, mf.data()) != hipSuccess) return bail("CU-masked FFT stream");
+    bool nomask = false;
+#ifdef RFA_AB_BUILD
+    // A/B builds (RFA_PIPE_NOMASK=1): no CU masks -- the state pass's workgroups share the FFT's CUs
+    // (co-resident beside an FFT workgroup compiled for fewer VGPRs, RFA_WIDE_WPE); the FFT streams
+    // get the higher priority
+    if (const char *d = std::getenv("RFA_PIPE_NOMASK")) nomask = std::atoi(d) != 0;
+#endif
+    if (nomask) {
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (hipStreamCreateWithPriority(&h->pipe_state, hipStreamNonBlocking, lo) != hipSuccess) return bail("state stream");
+        for (hipStream_t &fs : h->pipe_fft)
+            if (hipStreamCreateWithPriority(&fs, hipStreamNonBlocking, hi) != hipSuccess) return bail("FFT stream");
+    } else {
+        if (hipExtStreamCreateWithCUMask(&h->pipe_state, (uint32_t)words, ms.data()) != hipSuccess)
+            return bail("CU-masked state stream");
+        for (hipStream_t &fs : h->pipe_fft)
+            if (hipExtStreamCreateWithCUMask(&fs, (uint32_t)words, mf.data()) != hipSuccess)
+                return bail("CU-masked FFT stream");
+    }
     for (hipEvent_t *e : {&h->pipe_in, &h->pipe_fft_done[0], &h->pipe_fft_done[1], &h->pipe_state_done[0],
                           &h->pipe_state_done[1]})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return bail("pipeline events");
     h->pipe_cus = state_cus;
-    h->pipe_fft_cus = ncu - state_cus;
+    h->pipe_fft_cus = nomask ? ncu : ncu - state_cus;
     return RFA_OK;
 }
 

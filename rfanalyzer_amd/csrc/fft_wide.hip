@@ -469,7 +469,15 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
 // formats, one sub-FFT per workgroup, frame fits the exchange buffer; the
 // host launches a persistent grid and checks 16-byte alignment).
 template <int LOGM, int PT, int RS, int FMT, bool COMPLEX_OUT, int DIAG = 0, bool STG = false>
-__global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) fft_wide_kernel(FftLaunch a) {
+#ifndef RFA_WIDE_WPE
+#define RFA_WIDE_WPE 0  // A/B builds: waves per EU the wide kernels are compiled for (0: the launch bound's 4)
+#endif
+#if RFA_WIDE_WPE
+#define RFA_WIDE_ATTR __attribute__((amdgpu_waves_per_eu(RFA_WIDE_WPE, RFA_WIDE_WPE)))
+#else
+#define RFA_WIDE_ATTR
+#endif
+__global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4)) RFA_WIDE_ATTR fft_wide_kernel(FftLaunch a) {
     using G = WGeo<LOGM, PT>;
     constexpr int M = G::M;
     constexpr int BPS = (FMT == 0 || FMT == 1) ? 2 : (FMT == 2 ? 4 : 8);
