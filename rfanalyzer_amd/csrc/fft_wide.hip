@@ -34,6 +34,10 @@ namespace rfa {
 #ifndef RFA_RING_SC1
 #define RFA_RING_SC1 1  // 16-B ring tile stores write-through (profiles/r04/ring_store_sc1_ab.txt; A/B: 0)
 #endif
+#ifndef RFA_STG_OWN
+#define RFA_STG_OWN 1  // SPLIT halves staged wave-owned (stage_half_own), no item-start barrier (A/B: 0,
+                       // profiles/r06/stage_own_ab.txt)
+#endif
 #ifndef RFA_WIDE_KR1
 #define RFA_WIDE_KR1 0
 #endif
@@ -278,14 +282,18 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     // fit beside the PT points in the register budget (64 VGPRs at PT = 32)
     constexpr int C = (PT == 64 ? 16 : 8) / RS > 0 ? (PT == 64 ? 16 : 8) / RS : 1;
     constexpr int NCH = PT / C;
+    // SPLIT halves staged wave-owned (stage_half_own): wave w's slice, piece t at 64 t
+    constexpr bool OWN = RFA_STG_OWN && STG && JS < 0;
+    static_assert(!OWN || (G::THREADS == 1024 && PT == 32), "OWN: 16 waves, M / 16 samples of each half per wave");
+    const int ltid = OWN ? (tid >> 6) * (M / 16) + (tid & 63) : tid;
     auto lraw_t = [&] {  // this thread's samples in the staged frame (opaque base, see lds_opaque)
-        if constexpr (STG) return lds_opaque(lraw + tid);
+        if constexpr (STG) return lds_opaque(lraw + ltid);
         else return lraw;
     }();
     // the second sample of a point (x[m + M], region A under SPLIT: a negative element
     // offset) from its own base, so every ds_read_u16 takes an immediate offset
     auto lraw_t1 = [&] {
-        if constexpr (STG && RS == 2) return lds_opaque(lraw + tid + (JS != 0 ? JS : M));
+        if constexpr (STG && RS == 2) return lds_opaque(lraw + ltid + (JS != 0 ? JS : M));
         else return lraw_t;
     }();
     const rsrc_t w_rs = CW ? make_rsrc(cw, M * 16) : make_rsrc(window_il, M * RS * 4);
@@ -309,11 +317,12 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
         for (int q = 0; q < C; q++) {
             const int idx = c * C + q, b = idx >> 5, t = idx & 31;
             const int mo = G::TPF * b + (M / 32) * t;  // uniform part of m
+            const int mol = OWN ? 64 * t : mo;           // its place in the staged slice
 #pragma unroll
             for (int j = 0; j < RS; j++) {
                 if constexpr (STG && (QCH == 0 || c < QCH)) {  // frame (QCH: its first QCH chunks) staged in LDS
-                    if (STG && RS == 2 && j == 1) raw[s][q][j] = lraw_t1[mo];
-                    else raw[s][q][j] = lraw_t[mo + j * (JS != 0 ? JS : M)];
+                    if (STG && RS == 2 && j == 1) raw[s][q][j] = lraw_t1[mol];
+                    else raw[s][q][j] = lraw_t[mol + j * (JS != 0 ? JS : M)];
                 }
                 else raw[s][q][j] = buf_load_raw<FMT>(in_rs, tid * SB, (mo + j * M) * SB, planar_im);
             }
@@ -463,6 +472,34 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     }
 }
 
+// Wave-owned staging of one half of a 64 K 8-bit frame (SPLIT kernels, RFA_STG_OWN): wave w
+// stages exactly the samples its own threads read in the pre-stage -- sample 64 w + l + (M/32) t
+// of the half for lane l and t < 32, i.e. 32 pieces of 64 samples, (M/32) samples apart -- into
+// its own contiguous slice of the region (piece t at t * 64 samples).  Each 16-B lane of an LDS-DMA
+// instruction fetches from its own address, so 8 lanes take one piece and one instruction
+// eight.  The item-start wait is then the wave's own vmcnt: no barrier.
+template <int HALF_BYTES, int THREADS, int BPS, int STRIDE>
+__device__ __forceinline__ void stage_half_own(const void *src, float2 *buf) {
+    constexpr int NW = THREADS / 64, WB = HALF_BYTES / NW, PB = 64 * BPS, LPP = PB / 16, PPI = 64 / LPP;
+    constexpr int PER = WB / 1024;
+    static_assert(WB % 1024 == 0 && PB % 16 == 0 && PER * PPI * PB == WB, "whole pieces per instruction");
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const rsrc_t rs = make_rsrc(src, HALF_BYTES);
+    const unsigned base = (unsigned)(size_t)(__attribute__((address_space(3))) uint8_t *)(uint8_t *)buf + w * WB;
+    const int vo = (lane / LPP) * STRIDE * BPS + (lane % LPP) * 16;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+            "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "s"(base + j * 1024), "v"(vo), "s"(rs), "s"(j * PPI * STRIDE * BPS + w * PB)
+            : "memory");
+    }
+}
+
 // DIAG (profiling-only ablations, RFA_DIAG): 1 synthetic input (no input loads),
 // 2 no row stores, 4 no butterflies/twiddles, 8 no LDS exchanges, 16 no window loads.
 // STG: raw input staged through LDS by LDS-DMA one work item ahead (8/16-bit
@@ -567,8 +604,13 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     const int u0 = blockIdx.x;  // first item of this workgroup
     auto next_item = [&](int u) { return u + (int)gridDim.x; };
     // SPLIT: half 0 of a frame goes to region B, half 1 to region A
+    constexpr bool OWN = SPLIT && RFA_STG_OWN;
+    static_assert(!OWN || (PT == 32 && G::TPF == M / 32), "OWN: one pre-stage sample per thread per M/32");
     auto stage_half = [&](int f, int half) {
-        if constexpr (SPLIT)
+        if constexpr (OWN)
+            stage_half_own<HALF_BYTES, G::THREADS, BPS, M / 32>(
+                a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0), half ? buf : buf + QP);
+        else if constexpr (SPLIT)
             stage_frame<HALF_BYTES, G::THREADS>(a.in + (size_t)f * (size_t)a.frame_stride + (half ? HALF_BYTES : 0),
                                                 half ? buf : buf + QP);
     };
@@ -659,9 +701,15 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // this wave's pieces, then for every wave's (the barrier)
             // operations younger than the frame's LDS-DMA: the epilogue stores
             const int younger = pending_st;
-            if (younger >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if constexpr (OWN) {  // the wave's own pieces only: no barrier
+                if (younger >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+                else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            } else {
+                if (younger >= 63) asm volatile("s_waitcnt vmcnt(63) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            }
             stamp(u, 1);
         }
         if constexpr (RS == 1) {
