@@ -34,6 +34,13 @@ namespace rfa {
 #ifndef RFA_RING_SC1
 #define RFA_RING_SC1 1  // 16-B ring tile stores write-through (profiles/r04/ring_store_sc1_ab.txt; A/B: 0)
 #endif
+#ifndef RFA_WIN_UPFRONT
+#define RFA_WIN_UPFRONT 16  // residue 0's first 16 window pairs loaded into v[] up front (A/B: 0;
+                            // profiles/r06/residue_loop_window_ab.txt)
+#endif
+#ifndef RFA_RES_HOIST
+#define RFA_RES_HOIST 1  // the 64 K item loop instantiated per residue (A/B: 0; profiles/r06/residue_loop_window_ab.txt)
+#endif
 #ifndef RFA_STG_OWN
 #define RFA_STG_OWN 1  // SPLIT halves staged wave-owned (stage_half_own), no item-start barrier (A/B: 0,
                        // profiles/r06/stage_own_ab.txt)
@@ -426,6 +433,65 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
             }
         }
     };
+    // RFA_WIN_UPFRONT: residue 0 of a staged frame loads its first KU window pairs straight into
+    // v[] (the pre-stage's own output registers) before any arithmetic, so they are all in flight
+    // at once instead of two chunks; the samples come from LDS chunk by chunk, each point is the
+    // same mul + fma as below, and the remaining points go through the chunk pipeline (all 32 up
+    // front spill: 228 B of scratch)
+#if RFA_WIN_UPFRONT
+    // KU points' window pairs up front into v[], the rest through the chunk pipeline below
+    constexpr int KU = RFA_WIN_UPFRONT >= PT ? PT : RFA_WIN_UPFRONT;
+    constexpr bool WUP = STG && RS == 2 && R == 0 && !NOWIN && !CW && QCH == 0 && PT == 32 && KU % C == 0;
+    if constexpr (WUP) {
+        int zo;  // opaque zero: the scalar offsets are built here, not hoisted out of the item loop
+        asm volatile("s_mov_b32 %0, 0" : "=s"(zo));
+#pragma unroll
+        for (int idx = 0; idx < KU; idx++)
+            v[idx] = from_v(__builtin_bit_cast(
+                f2v, __builtin_amdgcn_raw_buffer_load_b64(w_rs, tid * 8, zo + (M / 32) * idx * 8, 0)));
+        constexpr int NU = KU / C;  // up-front chunks
+        if constexpr (NU < NCH) issue.template operator()<NU>();
+        typename Raw<FMT>::T rw[2][C][2];
+        auto ld = [&]<int c>() {
+#pragma unroll
+            for (int q = 0; q < C; q++) {
+                const int t = c * C + q, mol = OWN ? 64 * t : (M / 32) * t;
+                rw[c & 1][q][0] = lraw_t[mol];
+                rw[c & 1][q][1] = lraw_t1[mol];
+            }
+        };
+        ld.template operator()<0>();
+        [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+            (
+                [&] {
+                    if constexpr (Cs + 1 < NU) ld.template operator()<Cs + 1>();
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < C; q++) {
+                        const int i = Cs * C + q;
+                        const f2v x0 = to_v(convert_raw<FMT>(rw[Cs & 1][q][0])), x1 = to_v(convert_raw<FMT>(rw[Cs & 1][q][1]));
+                        const float w0 = v[i].x, w1 = v[i].y;
+                        v[i] = from_v(__builtin_elementwise_fma(x1, (f2v){w1, w1}, x0 * w0));
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NU>{});
+        [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
+            (
+                [&] {
+                    if constexpr (Cs >= NU) {
+                        if constexpr (Cs + 1 < NCH) issue.template operator()<Cs + 1>();
+                        __builtin_amdgcn_sched_barrier(0);
+                        compute.template operator()<Cs>();
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }(),
+                ...);
+        }(std::make_integer_sequence<int, NCH>{});
+        return;
+    }
+#endif
     [&]<int... Cs>(std::integer_sequence<int, Cs...>) {
         ((Cs < DIST && Cs < NCH ? issue.template operator()<Cs>() : void()), ...);
     }(std::make_integer_sequence<int, DIST>{});
@@ -654,7 +720,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
     // than the frame's LDS-DMA, so only the DMA and older operations are waited for)
     int pending_st = 0;
 
+#if RFA_RES_HOIST
+    auto body = [&]<int RF>(int u, int unext) {  // RF >= 0: every item of this loop is residue RF
+#else
     auto body = [&](int u, int unext) {
+#endif
         stamp(u, 0);
         // the lane index, opaque per item: the per-thread LDS bases derived from it are then
         // built inside the item, not hoisted out of the item loop (where they spill to scratch,
@@ -740,7 +810,11 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // W_RS^{j r} factors are compile-time rotations
             const int planar = planar_im;
             [&]<int... Rs>(std::integer_sequence<int, Rs...>) {
+#if RFA_RES_HOIST
+                (((RF >= 0 ? RF == Rs : r == Rs) ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, QST ? QN : JS,
+#else
                 ((r == Rs ? prestage<LOGM, PT, RS, FMT, Rs, STG, (DIAG & 16) != 0, QST ? QN : JS,
+#endif
                                      RS == 2 && Rs == 1 && FMT <= 2 && (DIAG & 16) == 0, QCH>(
                                 v, a.window_il, a.wide_tw, in_rs, tid, planar, lraw, a.window_cw)
                           : void()), ...);
@@ -929,11 +1003,34 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             stamp(u, 6);
         }
     };
+#if RFA_RES_HOIST
+    auto loop = [&]<int RF>() {
+        for (int u = u0; u < items; it_count++) {
+            const int un = next_item(u);
+            body.template operator()<RF>(u, un);
+            u = un;
+        }
+    };
+    // RFA_RES_HOIST: with a grid that is a multiple of 8 RS blocks every item of a
+    // workgroup has the same residue, so the item loop is instantiated per residue (register
+    // allocation per residue path, no per-item residue branch)
+    if constexpr (RS == 2 && !dif) {
+        if (gridDim.x % (8 * RS) == 0) {
+            if (((u0 % (8 * RS)) >> 3) == 0) loop.template operator()<0>();
+            else loop.template operator()<1>();
+        } else {
+            loop.template operator()<-1>();
+        }
+    } else {
+        loop.template operator()<-1>();
+    }
+#else
     for (int u = u0; u < items; it_count++) {
         const int un = next_item(u);
         body(u, un);
         u = un;
     }
+#endif
 }
 
 template <int LOGM, int PT, int RS, int FMT, bool CO, int DIAG = 0, bool STG = false>
