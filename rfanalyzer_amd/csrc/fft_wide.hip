@@ -41,6 +41,9 @@ namespace rfa {
 #ifndef RFA_RES_HOIST
 #define RFA_RES_HOIST 1  // the 64 K item loop instantiated per residue (A/B: 0; profiles/r06/residue_loop_window_ab.txt)
 #endif
+#ifndef RFA_STG_OWNQ
+#define RFA_STG_OWNQ 1  // QST's staged cf32 quarters (64 K f32) wave-owned too (A/B: 0; profiles/r06/f32_stage_own_ab.txt)
+#endif
 #ifndef RFA_STG_OWN
 #define RFA_STG_OWN 1  // SPLIT halves staged wave-owned (stage_half_own), no item-start barrier (A/B: 0,
                        // profiles/r06/stage_own_ab.txt)
@@ -290,9 +293,11 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     constexpr int C = (PT == 64 ? 16 : 8) / RS > 0 ? (PT == 64 ? 16 : 8) / RS : 1;
     constexpr int NCH = PT / C;
     // SPLIT halves staged wave-owned (stage_half_own): wave w's slice, piece t at 64 t
-    constexpr bool OWN = RFA_STG_OWN && STG && JS < 0;
+    // (RFA_STG_OWNQ: QST's two staged cf32 quarters too, QN / 16 samples of each per wave)
+    constexpr bool OWN = (RFA_STG_OWN && STG && JS < 0) || (RFA_STG_OWNQ && STG && QCH > 0 && RS == 2);
     static_assert(!OWN || (G::THREADS == 1024 && PT == 32), "OWN: 16 waves, M / 16 samples of each half per wave");
-    const int ltid = OWN ? (tid >> 6) * (M / 16) + (tid & 63) : tid;
+    constexpr int OWN_SLICE = QCH > 0 ? JS / 16 : M / 16;  // samples per wave slice
+    const int ltid = OWN ? (tid >> 6) * OWN_SLICE + (tid & 63) : tid;
     auto lraw_t = [&] {  // this thread's samples in the staged frame (opaque base, see lds_opaque)
         if constexpr (STG) return lds_opaque(lraw + ltid);
         else return lraw;
@@ -651,11 +656,17 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             }
         }
     };
+    constexpr bool OWNQ = QST && RFA_STG_OWNQ;
     auto stage_q = [&](int f) {  // QST: the two staged pieces of frame f
         if constexpr (QST) {
             const uint8_t *fb = a.in + (size_t)f * (size_t)a.frame_stride;
-            stage_frame<Q_BYTES, G::THREADS>(fb, buf);
-            stage_frame<Q_BYTES, G::THREADS>(fb + (size_t)M * 8, buf + QN);
+            if constexpr (OWNQ) {
+                stage_half_own<Q_BYTES, G::THREADS, 8, M / 32>(fb, buf);
+                stage_half_own<Q_BYTES, G::THREADS, 8, M / 32>(fb + (size_t)M * 8, buf + QN);
+            } else {
+                stage_frame<Q_BYTES, G::THREADS>(fb, buf);
+                stage_frame<Q_BYTES, G::THREADS>(fb + (size_t)M * 8, buf + QN);
+            }
         }
     };
     // frame of work item u (same mapping as body())
@@ -771,7 +782,7 @@ __global__ void __launch_bounds__((WGeo<LOGM, PT>::THREADS), (PT == 64 ? 2 : 4))
             // this wave's pieces, then for every wave's (the barrier)
             // operations younger than the frame's LDS-DMA: the epilogue stores
             const int younger = pending_st;
-            if constexpr (OWN) {  // the wave's own pieces only: no barrier
+            if constexpr (OWN || OWNQ) {  // the wave's own pieces only: no barrier
                 if (younger >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
                 else if (younger >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
