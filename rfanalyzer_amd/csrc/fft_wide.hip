@@ -444,7 +444,6 @@ __device__ __forceinline__ void prestage(float2 (&v)[PT], const float *window_il
     // same mul + fma as below, and the remaining points go through the chunk pipeline (all 32 up
     // front spill: 228 B of scratch)
 #if RFA_WIN_UPFRONT
-    // KU points' window pairs up front into v[], the rest through the chunk pipeline below
     constexpr int KU = RFA_WIN_UPFRONT >= PT ? PT : RFA_WIN_UPFRONT;
     constexpr bool WUP = STG && RS == 2 && R == 0 && !NOWIN && !CW && QCH == 0 && PT == 32 && KU % C == 0;
     if constexpr (WUP) {
@@ -543,12 +542,13 @@ __device__ __forceinline__ void stage_frame(const void *src, float2 *buf) {
     }
 }
 
-// Wave-owned staging of one half of a 64 K 8-bit frame (SPLIT kernels, RFA_STG_OWN): wave w
-// stages exactly the samples its own threads read in the pre-stage -- sample 64 w + l + (M/32) t
-// of the half for lane l and t < 32, i.e. 32 pieces of 64 samples, (M/32) samples apart -- into
-// its own contiguous slice of the region (piece t at t * 64 samples).  Each 16-B lane of an LDS-DMA
-// instruction fetches from its own address, so 8 lanes take one piece and one instruction
-// eight.  The item-start wait is then the wave's own vmcnt: no barrier.
+// Wave-owned staging of one half of a 64 K 8-bit frame (SPLIT kernels, RFA_STG_OWN) or of one of
+// the 64 K cf32 kernel's two staged quarters (QST, RFA_STG_OWNQ): wave w stages exactly the samples
+// its own threads read in the pre-stage -- sample 64 w + l + (M/32) t of the piece for lane l, i.e.
+// runs of 64 samples, (M/32) samples apart -- into its own contiguous slice of the region (run t at
+// t * 64 samples).  Each 16-B lane of an LDS-DMA instruction fetches from its own address, so
+// PB / 16 lanes take one run (8 for 8-bit IQ, 32 for cf32).  The item-start wait is then the
+// wave's own vmcnt: no barrier.
 template <int HALF_BYTES, int THREADS, int BPS, int STRIDE>
 __device__ __forceinline__ void stage_half_own(const void *src, float2 *buf) {
     constexpr int NW = THREADS / 64, WB = HALF_BYTES / NW, PB = 64 * BPS, LPP = PB / 16, PPI = 64 / LPP;
