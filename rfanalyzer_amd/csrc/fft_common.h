@@ -578,9 +578,8 @@ __device__ __forceinline__ void buf_store_f32x2(float2 x, rsrc_t rs, int voff, i
 // state_partial_kernel: pk = max, emi = the EMA started from -inf, b = the affine offset
 // of the EMA started from 0, restart = some frame was -inf).  Peak: FftProcessor.kt:241-242;
 // EMA (extension): the avg += alpha (x - avg) idiom of GlobalPerformanceData.kt:44-50.
-// Explicit fmaf: every kernel that forms a summary (state_partial / state_fused and the
-// wide kernel's in-grid units) rounds identically, so the result does not depend on
-// which of them computed a chunk.
+// Explicit fmaf: every kernel that forms a summary (state_partial / state_fused) rounds
+// identically, so the result does not depend on which of them computed a chunk.
 RFA_HD void state_step(float &pk, float &emi, float &b, bool &restart, float x, float al) {
     pk = fmaxf(pk, x);
     emi = (emi > -INFINITY) ? fmaf(al, x - emi, emi) : x;
